@@ -1,0 +1,1197 @@
+// gar_engine.cpp -- host state machine + C ABI (include/gar.h).
+//
+// The reference keeps, per channel, a chain of engine.Resampler stages
+// (constant.go:16-85) whose streaming state is history slices plus integer
+// counters (dft_stage.go:156-207, polyphase_stage.go:186-312,
+// dft_stage.go:488-554).  Here the *counters* are tracked on the host with the
+// reference's exact integer arithmetic -- so every call returns exactly the
+// reference's number of samples -- while the sample histories live in HBM as
+// interleaved [t][channel] rows and all sample arithmetic runs in HIP kernels
+// (gar_kernels.hip).  Channels in lockstep share one group and one launch.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "gar.h"
+#include "gar_design.hpp"
+#include "gar_kernels.hpp"
+#include "gar_plan.hpp"
+
+namespace gar {
+namespace {
+
+thread_local std::string g_err;
+
+struct DevError {
+    hipError_t e;
+    std::string what;
+};
+#define HIPCHK(x)                                                   \
+    do {                                                            \
+        hipError_t e_ = (x);                                        \
+        if (e_ != hipSuccess) throw DevError{e_, #x};               \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; cap = o.cap; o.p = nullptr; o.cap = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    void ensure(size_t bytes) {
+        if (bytes <= cap) return;
+        release();
+        const size_t nb = bytes + bytes / 4 + 256;
+        HIPCHK(hipMalloc(&p, nb));
+        cap = nb;
+    }
+    template <class T>
+    void upload(const std::vector<T>& v) {
+        ensure(sizeof(T) * std::max<size_t>(v.size(), 1));
+        if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Stage runtime: one engine design + its device plans, shared by all channels
+// (the reference designs the same filters once per channel, constant.go:57-70).
+// ---------------------------------------------------------------------------
+struct StageRT {
+    EngineDesign d;
+    bool f64 = false;
+    bool fused = false;
+    FirPeriodic compositeFir;
+    BgPlan fusedP, dftP, decimP;
+    DevBuf fusedA, fusedT, dftA, dftT, decimA, decimT;
+    BgDev fusedD{}, dftD{}, decimD{};
+    DevBuf pa, pb, pc, pd;
+    PolyDev polyD{};
+
+    int tc() const { return f64 ? 8 : 4; }
+};
+
+BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
+    BgDev d{};
+    d.f64 = p.f64 ? 1 : 0;
+    d.Pc = p.Pc; d.Qc = p.Qc; d.Kc = p.Kc; d.NS = p.NS; d.nrb = p.nrb;
+    d.ntasks = static_cast<int>(p.tasks.size());
+    d.ksplit = p.ksplit ? 1 : 0;
+    if (dry) return d;
+    if (p.f64) A.upload(p.A64); else A.upload(p.A32);
+    std::vector<int> t;
+    for (const auto& k : p.tasks) { t.push_back(k.rb); t.push_back(k.k0); t.push_back(k.ns); t.push_back(k.ks); t.push_back(k.nks); }
+    T.upload(t);
+    d.A = A.p;
+    d.tasks = static_cast<const int*>(T.p);
+    return d;
+}
+
+template <class T>
+void uploadBank(const std::vector<double>& v, DevBuf& b) {
+    std::vector<T> c(v.begin(), v.end());
+    b.upload(c);
+}
+
+bool buildStage(StageRT& s, bool f64, bool dry, std::string& err) {
+    s.f64 = f64;
+    const EngineDesign& d = s.d;
+    if (d.kind == EngineKind::Cubic) { err = "QualityQuick cubic stage is not supported on the GPU path yet"; return false; }
+    if (d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) {
+        if (!buildBgPlan(firFromDft(d.dft), f64, s.dftP)) { err = "DFT plan"; return false; }
+        s.dftD = uploadPlan(s.dftP, s.dftA, s.dftT, dry);
+    }
+    if (d.kind == EngineKind::Decim) {
+        if (!buildBgPlan(firFromDecim(d.decim), f64, s.decimP)) { err = "decimator plan"; return false; }
+        s.decimD = uploadPlan(s.decimP, s.decimA, s.decimT, dry);
+    }
+    if (d.kind == EngineKind::DftPoly) {
+        if (firComposite(d.dft, d.poly, s.compositeFir) && buildBgPlan(s.compositeFir, f64, s.fusedP)) {
+            s.fused = true;
+            s.fusedD = uploadPlan(s.fusedP, s.fusedA, s.fusedT, dry);
+        }
+        PolyDev& p = s.polyD;
+        p.f64 = f64 ? 1 : 0;
+        p.L = d.poly.L;
+        p.T = d.poly.taps;
+        p.step = d.poly.step;
+        if (!dry) {
+            if (f64) {
+                uploadBank<double>(d.poly.a, s.pa); uploadBank<double>(d.poly.b, s.pb);
+                uploadBank<double>(d.poly.cc, s.pc); uploadBank<double>(d.poly.d, s.pd);
+            } else {
+                uploadBank<float>(d.poly.a, s.pa); uploadBank<float>(d.poly.b, s.pb);
+                uploadBank<float>(d.poly.cc, s.pc); uploadBank<float>(d.poly.d, s.pd);
+            }
+            p.a = s.pa.p; p.b = s.pb.p; p.c = s.pc.p; p.d = s.pd.p;
+        }
+    }
+    return true;
+}
+
+// StageAdapter.GetLatency (internal/engine/stage_adapter.go:43-57)
+int stageLatency(const EngineDesign& d) {
+    int lat = 0;
+    if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1)
+        lat += (d.dft.taps * d.dft.factor) / 2;
+    if (d.kind == EngineKind::DftPoly) lat += d.poly.taps / 2;
+    return lat;
+}
+
+// ---------------------------------------------------------------------------
+// Per-stage streaming counters (exact reference integer semantics).
+// ---------------------------------------------------------------------------
+struct Counters {
+    bool staged = false;       // DFT+poly engine running stage-by-stage (else fused)
+    int64_t x_count = 0;       // samples appended to the stage input stream
+    int64_t dft_hist = 0;      // len(DFTStage.history)
+    int64_t poly_hist = 0;     // len(PolyphaseStage.history)
+    int64_t at = 0;            // PolyphaseStage.at
+    int64_t u_base = 0;        // poly-stream index of PolyphaseStage.history[0]
+    int64_t u_count = 0;       // samples appended to the poly stream
+    int64_t dec_hist = 0;      // len(DFTDecimationStage.history)
+    int dec_phase = 0;         // DFTDecimationStage.decimPhase
+    int64_t y_count = 0;       // samples emitted
+};
+
+// DFTStage.processZeroCopy counts (dft_stage.go:156-207)
+int64_t cntDft(Counters& s, const DftBank& b, int64_t n) {
+    if (b.factor == 1) return n;
+    if (n == 0) return 0;
+    s.x_count += n;
+    s.dft_hist += n;
+    if (s.dft_hist < b.taps) return 0;
+    const int64_t p = s.dft_hist - b.taps + 1;
+    s.dft_hist -= p;
+    return p * b.factor;
+}
+
+// PolyphaseStage.processZeroCopy counts (polyphase_stage.go:186-312)
+int64_t cntPoly(Counters& s, const PolyBank& b, int64_t m, bool& quirk) {
+    if (m == 0) return 0;
+    s.poly_hist += m;
+    s.u_count += m;
+    const int64_t numIn = s.poly_hist - b.taps + 1;
+    if (numIn <= 0) return 0;
+    const int64_t L = b.L;
+    const int64_t limit = (numIn * L) << 16;
+    const int64_t nout = (limit - s.at + b.step - 1) / b.step;
+    if (nout <= 0) return 0;
+    const int64_t at = s.at + nout * b.step;
+    const int64_t consumed = (at >> 16) / L;
+    if (consumed > 0 && consumed <= s.poly_hist) {
+        s.poly_hist -= consumed;
+        s.u_base += consumed;
+    } else if (consumed > s.poly_hist) {
+        quirk = true;  // history left untrimmed, `at` still rebased (polyphase_stage.go:300-307)
+    }
+    s.at = at - ((consumed * L) << 16);
+    return nout;
+}
+
+// DFTDecimationStage.processZeroCopy counts (dft_stage.go:488-554)
+int64_t cntDecim(Counters& s, const DecimBank& b, int64_t n) {
+    if (b.factor == 1) return n;
+    if (n == 0) return 0;
+    s.x_count += n;
+    s.dec_hist += n;
+    if (s.dec_hist < b.taps) return 0;
+    const int64_t nf = s.dec_hist - b.taps + 1;
+    const int64_t nout = s.dec_phase < nf ? (nf - s.dec_phase + b.factor - 1) / b.factor : 0;
+    if (nout == 0) return 0;  // early return leaves history and phase untouched (dft_stage.go:516-518)
+    s.dec_phase = static_cast<int>(((s.dec_phase - nf) % b.factor + b.factor) % b.factor);
+    s.dec_hist -= nf;
+    return nout;
+}
+
+// ---------------------------------------------------------------------------
+struct Hist {
+    DevBuf buf[2];
+    int cur = 0;
+    int64_t base = 0, len = 0;
+    void* ptr() const { return buf[cur].p; }
+    void clear() { base = 0; len = 0; }
+};
+
+struct StageDev {
+    Hist xh;  // stage input stream history
+    Hist uh;  // poly-stream history (staged DFT+poly)
+};
+
+struct InView {
+    const void* p = nullptr;
+    int64_t fs = 0, cs = 0;
+    int f64 = 0;
+    int64_t n = 0;
+    bool zeros = false;
+};
+
+struct OutView {
+    void* p = nullptr;
+    int64_t fs = 0, cs = 0;
+    int f64 = 0;
+};
+
+struct Group {
+    int c0 = 0, C = 1;
+    std::vector<Counters> cnt;
+    std::vector<StageDev> dev;
+    std::vector<DevBuf> tmp;   // per stage-boundary output buffers
+    DevBuf utmp;               // staged DFT output (u) scratch
+};
+
+}  // namespace
+}  // namespace gar
+
+struct gar_resampler {
+    bool newPath = true;
+    int channels = 1;      // total (streams * channels for a batch)
+    double ratio = 1.0;
+    bool f64 = true;       // compute dtype
+    bool dry = false;
+    int device = 0;
+    bool engineF32Io = false;
+    hipStream_t stream = nullptr;
+    gar_config cfg{};
+    std::vector<std::unique_ptr<gar::StageRT>> stages;
+    std::vector<gar::Group> groups;
+    gar::DevBuf inStage, outStage;
+    std::vector<int64_t> scratchSizes;
+};
+
+namespace gar {
+namespace {
+
+using Handle = gar_resampler;
+
+struct Ctx {
+    Handle* h;
+    Group* g;
+    hipStream_t s;
+    bool launch;
+};
+
+SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
+    SrcDesc s{};
+    s.hist = hs.ptr();
+    s.hist_base = hs.base;
+    s.hist_len = hs.len;
+    s.hist_ld = C;
+    s.in = in.zeros ? nullptr : in.p;
+    s.in_base = x0;
+    s.in_len = in.zeros ? 0 : in.n;
+    s.in_fs = in.fs;
+    s.in_cs = in.cs;
+    s.in_f64 = in.f64;
+    s.valid_end = in.zeros ? x0 : x0 + in.n;
+    return s;
+}
+
+OutDesc mkOut(const OutView& o, int64_t o0, int64_t n) {
+    OutDesc d{};
+    d.out = o.p;
+    d.o0 = o0;
+    d.fs = o.fs;
+    d.cs = o.cs;
+    d.f64 = o.f64;
+    d.o_lo = o0;
+    d.o_hi = o0 + n;
+    return d;
+}
+
+void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
+    const int C = x.g->C;
+    const int tc = x.h->f64 ? 8 : 4;
+    if (k1 < k0) k1 = k0;
+    if (!x.launch) { hs.base = k0; hs.len = k1 - k0; return; }
+    const int other = 1 - hs.cur;
+    hs.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(k1 - k0, 1)) * C * tc);
+    HIPCHK(launchGather(x.h->f64, src, hs.buf[other].p, k0, k1 - k0, C, x.s));
+    hs.cur = other;
+    hs.base = k0;
+    hs.len = k1 - k0;
+}
+
+// FUSED -> STAGED: rebuild the poly-stream history u[u_base, u_count) from x by
+// the DFT plan and keep the DFT's own history x[x_count - dft_hist, x_count).
+void materialize(Ctx& x, StageRT& rt, Counters& c, StageDev& dv, const SrcDesc& xsrc) {
+    const int C = x.g->C;
+    const int tc = rt.tc();
+    if (x.launch) {
+        Hist& uh = dv.uh;
+        const int other = 1 - uh.cur;
+        const int64_t n = c.u_count - c.u_base;
+        uh.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(n, 1)) * C * tc);
+        OutView ov{uh.buf[other].p, C, 1, rt.f64 ? 1 : 0};
+        HIPCHK(launchBg(rt.dftD, xsrc, mkOut(ov, c.u_base, n), C, x.s));
+        uh.cur = other;
+        uh.base = c.u_base;
+        uh.len = n;
+    } else {
+        dv.uh.base = c.u_base;
+        dv.uh.len = c.u_count - c.u_base;
+    }
+    hist_update(x, dv.xh, xsrc, c.x_count - c.dft_hist, c.x_count);
+    c.staged = true;
+}
+
+// engine.Resampler.ProcessZeroCopy for one stage (resampler.go:232-272).
+int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
+    StageRT& rt = *x.h->stages[si];
+    Counters& c = x.g->cnt[si];
+    StageDev& dv = x.g->dev[si];
+    const int C = x.g->C;
+    const EngineDesign& d = rt.d;
+    const int64_t n = in.n;
+    if (n == 0) return 0;
+    switch (d.kind) {
+        case EngineKind::Passthrough: {
+            if (x.launch && !in.zeros)
+                HIPCHK(launchCopy(in.p, in.f64, in.fs, in.cs, out.p, out.f64, out.fs, out.cs, n, C, x.s));
+            c.y_count += n;
+            return n;
+        }
+        case EngineKind::DftOnly: {
+            const int64_t x0 = c.x_count;
+            const int64_t y0 = c.y_count;
+            const int64_t nout = cntDft(c, d.dft, n);
+            const SrcDesc src = mkSrc(dv.xh, C, x0, in);
+            if (x.launch && nout > 0) HIPCHK(launchBg(rt.dftD, src, mkOut(out, y0, nout), C, x.s));
+            hist_update(x, dv.xh, src, c.x_count - c.dft_hist, c.x_count);
+            c.y_count += nout;
+            return nout;
+        }
+        case EngineKind::Decim: {
+            const int64_t x0 = c.x_count;
+            const int64_t y0 = c.y_count;
+            const int64_t nout = cntDecim(c, d.decim, n);
+            const SrcDesc src = mkSrc(dv.xh, C, x0, in);
+            if (x.launch && nout > 0) HIPCHK(launchBg(rt.decimD, src, mkOut(out, y0, nout), C, x.s));
+            hist_update(x, dv.xh, src, c.x_count - c.dec_hist, c.x_count);
+            c.y_count += nout;
+            return nout;
+        }
+        case EngineKind::DftPoly: {
+            const int64_t x0 = c.x_count;
+            const int64_t y0 = c.y_count;
+            const Counters before = c;
+            const SrcDesc xsrc = mkSrc(dv.xh, C, x0, in);
+            const int64_t nu = cntDft(c, d.dft, n);
+            bool quirk = false;
+            const int64_t nout = cntPoly(c, d.poly, nu, quirk);
+            if (!c.staged) {
+                // Fused: DFT x2 and polyphase composed into one MFMA FIR over x.
+                if (x.launch && nout > 0) HIPCHK(launchBg(rt.fusedD, xsrc, mkOut(out, y0, nout), C, x.s));
+                if (quirk) {
+                    materialize(x, rt, c, dv, xsrc);
+                } else {
+                    hist_update(x, dv.xh, xsrc, c.u_base / 2, c.x_count);
+                }
+            } else {
+                // Staged: DFT (MFMA FIR) into u scratch, polyphase with live cubic interpolation.
+                const int64_t p0 = before.x_count - before.dft_hist;   // DFT positions done before
+                const int64_t dy0 = p0 * d.dft.factor;
+                InView uin;
+                if (x.launch) {
+                    x.g->utmp.ensure(static_cast<size_t>(std::max<int64_t>(nu, 1)) * C * rt.tc());
+                    if (nu > 0) {
+                        OutView uv{x.g->utmp.p, C, 1, rt.f64 ? 1 : 0};
+                        HIPCHK(launchBg(rt.dftD, xsrc, mkOut(uv, dy0, nu), C, x.s));
+                    }
+                }
+                uin.p = x.g->utmp.p; uin.fs = C; uin.cs = 1; uin.f64 = rt.f64 ? 1 : 0; uin.n = nu;
+                const SrcDesc usrc = mkSrc(dv.uh, C, before.u_count, uin);
+                if (x.launch && nout > 0) {
+                    PolyDev p = rt.polyD;
+                    p.at0 = before.at;
+                    p.u_base = before.u_base;
+                    HIPCHK(launchPoly(p, usrc, mkOut(out, y0, nout), nout, C, x.s));
+                }
+                hist_update(x, dv.xh, xsrc, c.x_count - c.dft_hist, c.x_count);
+                if (nu > 0) hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
+            }
+            c.y_count += nout;
+            return nout;
+        }
+        default:
+            throw DevError{hipErrorNotSupported, "unsupported stage"};
+    }
+}
+
+// engine.Resampler.Flush for one stage (resampler.go:275-322).
+int64_t stageFlush(Ctx& x, int si, const OutView& out) {
+    StageRT& rt = *x.h->stages[si];
+    Counters& c = x.g->cnt[si];
+    StageDev& dv = x.g->dev[si];
+    const int C = x.g->C;
+    const EngineDesign& d = rt.d;
+    InView z;
+    z.zeros = true;
+    switch (d.kind) {
+        case EngineKind::Passthrough:
+            return 0;
+        case EngineKind::DftOnly:
+            if (c.dft_hist == 0) return 0;
+            z.n = d.dft.taps;
+            return stageProcess(x, si, z, out);
+        case EngineKind::Decim:
+            if (c.dec_hist == 0) return 0;
+            z.n = d.decim.taps;
+            return stageProcess(x, si, z, out);
+        case EngineKind::DftPoly: {
+            if (!c.staged) {
+                InView none;
+                none.zeros = true;
+                const SrcDesc xsrc = mkSrc(dv.xh, C, c.x_count, none);
+                materialize(x, rt, c, dv, xsrc);
+            }
+            int64_t total = 0;
+            // DFTStage.Flush -> PolyphaseStage.Process(intermediate)
+            if (c.dft_hist > 0) {
+                z.n = d.dft.taps;
+                total += stageProcess(x, si, z, out);
+            }
+            // PolyphaseStage.Flush: tapsPerPhase zeros into the poly stream
+            if (c.poly_hist > 0) {
+                const int64_t y0 = c.y_count;
+                const Counters before = c;
+                bool quirk = false;
+                const int64_t nout = cntPoly(c, d.poly, d.poly.taps, quirk);
+                InView uz;
+                uz.zeros = true;
+                uz.n = d.poly.taps;
+                const SrcDesc usrc = mkSrc(dv.uh, C, before.u_count, uz);
+                OutView o2 = out;
+                if (x.launch && nout > 0) {
+                    const int es = out.f64 ? 8 : 4;
+                    o2.p = static_cast<char*>(out.p) + total * out.fs * es;
+                    PolyDev p = rt.polyD;
+                    p.at0 = before.at;
+                    p.u_base = before.u_base;
+                    HIPCHK(launchPoly(p, usrc, mkOut(o2, y0, nout), nout, C, x.s));
+                }
+                hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
+                c.y_count += nout;
+                total += nout;
+            }
+            return total;
+        }
+        default:
+            return 0;
+    }
+}
+
+OutView offsetView(const OutView& o, int64_t rows) {
+    OutView r = o;
+    if (o.p) r.p = static_cast<char*>(o.p) + rows * o.fs * (o.f64 ? 8 : 4);
+    return r;
+}
+
+// constantRateResampler.processChannel[Into] (constant.go:255-345): the whole
+// chain; sizes[i] = samples produced by stage i (buffer i+1).
+int64_t chainProcess(Ctx& x, const InView& in, const OutView& out, std::vector<int64_t>& sizes) {
+    const int ns = static_cast<int>(x.h->stages.size());
+    sizes.assign(ns, 0);
+    if (ns == 0) {  // ratio within 0.1% of 1: no stages, the ring buffer passes input through
+        if (x.launch && in.n > 0)
+            HIPCHK(launchCopy(in.p, in.f64, in.fs, in.cs, out.p, out.f64, out.fs, out.cs, in.n, x.g->C, x.s));
+        return in.n;
+    }
+    InView cur = in;
+    for (int i = 0; i < ns; ++i) {
+        const bool last = i == ns - 1;
+        OutView o = out;
+        if (!last) {
+            const int tc = x.h->f64 ? 8 : 4;
+            if (x.launch) {
+                x.g->tmp[i].ensure(static_cast<size_t>(std::max<int64_t>(x.h->scratchSizes[i], 1)) * x.g->C * tc);
+                o = OutView{x.g->tmp[i].p, x.g->C, 1, x.h->f64 ? 1 : 0};
+            }
+        }
+        int64_t m = 0;
+        if (cur.n >= 1) m = stageProcess(x, i, cur, o);  // Available() >= GetMinInput() (constant.go:277,314)
+        sizes[i] = m;
+        InView nx;
+        nx.p = o.p; nx.fs = o.fs; nx.cs = o.cs; nx.f64 = o.f64; nx.n = m;
+        cur = nx;
+    }
+    return cur.n;
+}
+
+// flushChannel (constant.go:360-386)
+int64_t chainFlush(Ctx& x, const OutView& out, std::vector<int64_t>& sizes) {
+    const int ns = static_cast<int>(x.h->stages.size());
+    sizes.assign(ns, 0);
+    if (ns == 0) return 0;
+    InView pending;  // previous stage's flushed tail
+    for (int i = 0; i < ns; ++i) {
+        const bool last = i == ns - 1;
+        OutView o = out;
+        if (!last && x.launch) {
+            const int tc = x.h->f64 ? 8 : 4;
+            x.g->tmp[i].ensure(static_cast<size_t>(std::max<int64_t>(x.h->scratchSizes[i], 1)) * x.g->C * tc);
+            o = OutView{x.g->tmp[i].p, x.g->C, 1, x.h->f64 ? 1 : 0};
+        }
+        int64_t m = 0;
+        if (pending.n > 0) m += stageProcess(x, i, pending, o);
+        m += stageFlush(x, i, offsetView(o, m));
+        sizes[i] = m;
+        InView nx;
+        nx.p = o.p; nx.fs = o.fs; nx.cs = o.cs; nx.f64 = o.f64; nx.n = m;
+        pending = nx;
+    }
+    return pending.n;
+}
+
+Group* groupOf(Handle* h, int ch) {
+    for (auto& g : h->groups)
+        if (ch >= g.c0 && ch < g.c0 + g.C) return &g;
+    return nullptr;
+}
+
+Group freshGroup(Handle* h, int c0, int C) {
+    Group g;
+    g.c0 = c0;
+    g.C = C;
+    const size_t ns = h->stages.size();
+    g.cnt.assign(ns, Counters());
+    g.dev.resize(ns);
+    g.tmp.resize(ns);
+    for (size_t i = 0; i < ns; ++i)
+        if (!h->stages[i]->fused) g.cnt[i].staged = true;
+    return g;
+}
+
+// Copy channels [k0, k0+kc) of group g into a new group (Process on channel 0
+// of a multi-channel handle advances only that channel, constant.go:88-95).
+Group splitCopy(Handle* h, Group& g, int k0, int kc) {
+    Group ng = freshGroup(h, g.c0 + k0, kc);
+    const int tc = h->f64 ? 8 : 4;
+    for (size_t i = 0; i < h->stages.size(); ++i) {
+        ng.cnt[i] = g.cnt[i];
+        Hist* src[2] = {&g.dev[i].xh, &g.dev[i].uh};
+        Hist* dst[2] = {&ng.dev[i].xh, &ng.dev[i].uh};
+        for (int k = 0; k < 2; ++k) {
+            dst[k]->base = src[k]->base;
+            dst[k]->len = src[k]->len;
+            if (!h->dry && src[k]->len > 0) {
+                dst[k]->buf[0].ensure(static_cast<size_t>(src[k]->len) * kc * tc);
+                const char* sp = static_cast<const char*>(src[k]->ptr()) + static_cast<size_t>(k0) * tc;
+                HIPCHK(launchCopy(sp, h->f64, g.C, 1, dst[k]->buf[0].p, h->f64, kc, 1, src[k]->len, kc, h->stream));
+            }
+        }
+    }
+    return ng;
+}
+
+void isolate(Handle* h, int ch) {
+    Group* g = groupOf(h, ch);
+    if (!g || g->C == 1) return;
+    std::vector<Group> out;
+    for (auto& gg : h->groups) {
+        if (&gg != g) { out.push_back(std::move(gg)); continue; }
+        const int k = ch - gg.c0;
+        if (k > 0) out.push_back(splitCopy(h, gg, 0, k));
+        out.push_back(splitCopy(h, gg, k, 1));
+        if (k + 1 < gg.C) out.push_back(splitCopy(h, gg, k + 1, gg.C - k - 1));
+    }
+    if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+    h->groups = std::move(out);
+}
+
+// Dry-run a process (or flush) on copies of the group counters.
+int64_t simulate(Handle* h, Group& g, int64_t n, bool flush, std::vector<int64_t>& sizes) {
+    Group sim;
+    sim.c0 = g.c0;
+    sim.C = g.C;
+    sim.cnt = g.cnt;
+    sim.dev.resize(g.dev.size());
+    for (size_t i = 0; i < g.dev.size(); ++i) {
+        sim.dev[i].xh.base = g.dev[i].xh.base; sim.dev[i].xh.len = g.dev[i].xh.len;
+        sim.dev[i].uh.base = g.dev[i].uh.base; sim.dev[i].uh.len = g.dev[i].uh.len;
+    }
+    Ctx x{h, &sim, nullptr, false};
+    InView in;
+    in.n = n;
+    OutView o;
+    return flush ? chainFlush(x, o, sizes) : chainProcess(x, in, o, sizes);
+}
+
+// Run one group for real: sizes first (so scratch can be sized), then launches.
+int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool flush, hipStream_t s,
+                 int64_t cap, gar_status& st) {
+    std::vector<int64_t> sizes;
+    const int64_t n = simulate(h, g, in.n, flush, sizes);
+    if (n > cap) { st = GAR_ERR_BUFFER_TOO_SMALL; return n; }
+    st = GAR_OK;
+    if (h->dry) {
+        Ctx x{h, &g, nullptr, false};
+        std::vector<int64_t> s2;
+        OutView o;
+        if (flush) chainFlush(x, o, s2); else chainProcess(x, in, o, s2);
+        return n;
+    }
+    h->scratchSizes = sizes;
+    Ctx x{h, &g, s, true};
+    std::vector<int64_t> s2;
+    const int64_t got = flush ? chainFlush(x, out, s2) : chainProcess(x, in, out, s2);
+    if (got != n) { st = GAR_ERR_INTERNAL; g_err = "size mismatch between count and launch"; }
+    return got;
+}
+
+gar_status guard(gar_status s, const char* msg) {
+    if (s != GAR_OK) g_err = msg;
+    return s;
+}
+
+template <class F>
+gar_status wrap(F&& f) {
+    try {
+        return f();
+    } catch (const DevError& e) {
+        g_err = std::string("HIP error ") + hipGetErrorString(e.e) + " at " + e.what;
+        return GAR_ERR_DEVICE;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return GAR_ERR_INTERNAL;
+    }
+}
+
+// Precision carried by a preset (resample.go:217-267).
+gar_quality_spec presetSpec(int32_t preset) {
+    gar_quality_spec q{};
+    switch (preset) {
+        case GAR_QUALITY_QUICK: q = {GAR_QUALITY_QUICK, 8, 50.0, 0.7, 1.0, 0}; break;
+        case GAR_QUALITY_LOW: q = {GAR_QUALITY_LOW, 16, 50.0, 0.80, 0.95, 0}; break;
+        case GAR_QUALITY_MEDIUM: q = {GAR_QUALITY_MEDIUM, 16, 50.0, 0.90, 0.98, 0}; break;
+        case GAR_QUALITY_HIGH: q = {GAR_QUALITY_HIGH, 24, 50.0, 0.95, 0.99, 0}; break;
+        case GAR_QUALITY_VERYHIGH: q = {GAR_QUALITY_VERYHIGH, 32, 50.0, 0.99, 0.995, 0}; break;
+        default: q = {GAR_QUALITY_MEDIUM, 0, 0, 0, 0, 0}; break;
+    }
+    return q;
+}
+
+gar_status validate(const gar_config* c) {
+    if (!c) return guard(GAR_ERR_INVALID_CONFIG, "invalid resampler configuration: config is nil");
+    if (!(c->input_rate > 0) || !(c->output_rate > 0))
+        return guard(GAR_ERR_INVALID_CONFIG, "invalid resampler configuration: sample rates must be positive");
+    if (c->channels < 1) return guard(GAR_ERR_INVALID_CONFIG, "invalid resampler configuration: channels must be at least 1");
+    if (c->channels > 256) return guard(GAR_ERR_INVALID_CONFIG, "invalid resampler configuration: too many channels (max 256)");
+    const double r = c->output_rate / c->input_rate;
+    if (r < 1.0 / 256.0 || r > 256.0)
+        return guard(GAR_ERR_INVALID_CONFIG, "invalid resampler configuration: resampling ratio out of range");
+    const gar_quality_spec& q = c->quality;
+    if (q.preset == GAR_QUALITY_CUSTOM) {
+        if (q.precision < 8 || q.precision > 33) return guard(GAR_ERR_INVALID_CONFIG, "precision must be 8-33 bits");
+        if (q.phase_response < 0 || q.phase_response > 100) return guard(GAR_ERR_INVALID_CONFIG, "phase response must be 0-100");
+        if (q.passband_end <= 0 || q.passband_end >= 1) return guard(GAR_ERR_INVALID_CONFIG, "passband end must be in (0, 1)");
+        if (q.stopband_begin <= q.passband_end || q.stopband_begin > 1)
+            return guard(GAR_ERR_INVALID_CONFIG, "stopband begin must be in (passband_end, 1]");
+    }
+    return GAR_OK;
+}
+
+gar_status initDevice(Handle* h) {
+    if (h->dry) return GAR_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= h->device) {
+        g_err = "no HIP device visible (the GPU path requires an MI355X / gfx950)";
+        return GAR_ERR_DEVICE;
+    }
+    HIPCHK(hipSetDevice(h->device));
+    HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    return GAR_OK;
+}
+
+gar_status addStage(Handle* h, double inRate, double outRate, Quality q) {
+    auto rt = std::make_unique<StageRT>();
+    std::string err;
+    if (!designEngine(inRate, outRate, q, rt->d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
+    if (!buildStage(*rt, h->f64, h->dry, err)) {
+        g_err = err;
+        return rt->d.kind == EngineKind::Cubic ? GAR_ERR_NOT_SUPPORTED : GAR_ERR_INTERNAL;
+    }
+    h->stages.push_back(std::move(rt));
+    return GAR_OK;
+}
+
+gar_status newCommon(gar_config* cfg, int32_t nstreams, gar_resampler** out) {
+    if (!out) return guard(GAR_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    gar_status s = validate(cfg);
+    if (s != GAR_OK) return s;
+    if (nstreams < 1) return guard(GAR_ERR_INVALID_CONFIG, "n_streams must be >= 1");
+    if (cfg->quality.preset != GAR_QUALITY_CUSTOM) cfg->quality = presetSpec(cfg->quality.preset);
+    auto h = std::make_unique<Handle>();
+    h->newPath = true;
+    h->cfg = *cfg;
+    h->channels = cfg->channels * nstreams;
+    h->ratio = cfg->output_rate / cfg->input_rate;
+    h->f64 = cfg->compute_dtype != GAR_F32;
+    h->dry = cfg->dry_run != 0;
+    h->device = cfg->device;
+    return wrap([&]() -> gar_status {
+        gar_status st = initDevice(h.get());
+        if (st != GAR_OK) return st;
+        const int prec = cfg->quality.precision;
+        const std::vector<StageSpec> specs = buildPipeline(h->ratio, prec);
+        for (const StageSpec& sp : specs) {
+            // createStage -> engine.NewResampler[float64](48000, 48000*ratio, q) (stages.go:54-70)
+            if (sp.type == StageType::Cubic) {
+                g_err = "QualityQuick (cubic) pipelines are not supported on the GPU path yet";
+                return GAR_ERR_NOT_SUPPORTED;
+            }
+            const double ir = 48000.0;
+            st = addStage(h.get(), ir, ir * sp.ratio, precisionToEngineQuality(prec));
+            if (st != GAR_OK) return st;
+        }
+        h->groups.push_back(freshGroup(h.get(), 0, h->channels));
+        *out = h.release();
+        return GAR_OK;
+    });
+}
+
+int64_t estimate(const Handle* h, int64_t n) {
+    return static_cast<int64_t>(static_cast<double>(n) * h->ratio) + 64;
+}
+
+// H2D a host vector into the input staging buffer.
+InView stageIn(Handle* h, const void* in, int64_t n, int f64) {
+    InView v;
+    v.n = n;
+    v.f64 = f64;
+    v.fs = 1;
+    v.cs = 0;
+    if (h->dry || n == 0) return v;
+    const size_t es = f64 ? 8 : 4;
+    h->inStage.ensure(n * es);
+    HIPCHK(hipMemcpyAsync(h->inStage.p, in, n * es, hipMemcpyHostToDevice, h->stream));
+    v.p = h->inStage.p;
+    return v;
+}
+
+template <class T>
+gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t cap, int64_t* nOut, bool flush,
+                    bool intoSemantics) {
+    if (!h) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
+    if (ch < 0 || ch >= h->channels) return guard(GAR_ERR_INVALID_ARGUMENT, "channel out of range");
+    if (nOut) *nOut = 0;
+    if (!flush && n < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
+    if (!flush && intoSemantics && cap < estimate(h, n)) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+    const int f64 = sizeof(T) == 8 ? 1 : 0;
+    return wrap([&]() -> gar_status {
+        isolate(h, ch);
+        Group* g = groupOf(h, ch);
+        std::vector<int64_t> sizes;
+        const int64_t need = simulate(h, *g, flush ? 0 : n, flush, sizes);
+        if (need > cap) {
+            if (intoSemantics && !flush) { g_err = "EstimateOutput underestimated actual output length"; return GAR_ERR_INTERNAL; }
+            return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+        }
+        const InView iv = flush ? InView() : stageIn(h, in, n, f64);
+        OutView ov;
+        ov.fs = 1;
+        ov.cs = 0;
+        ov.f64 = f64;
+        if (!h->dry) {
+            h->outStage.ensure(std::max<int64_t>(need, 1) * sizeof(T));
+            ov.p = h->outStage.p;
+        }
+        gar_status st;
+        const int64_t got = runGroup(h, *g, iv, ov, flush, h->stream, cap, st);
+        if (st != GAR_OK) return st;
+        if (!h->dry && got > 0) HIPCHK(hipMemcpyAsync(out, h->outStage.p, got * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        if (nOut) *nOut = got;
+        return GAR_OK;
+    });
+}
+
+}  // namespace
+}  // namespace gar
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace gar;
+
+extern "C" {
+
+gar_status gar_config_validate(const gar_config* cfg) { return validate(cfg); }
+
+gar_quality_spec gar_preset_spec(int32_t preset) { return presetSpec(preset); }
+
+gar_status gar_new(gar_config* cfg, gar_resampler** out) { return newCommon(cfg, 1, out); }
+
+gar_status gar_new_batch(gar_config* cfg, int32_t n_streams, gar_resampler** out) {
+    return newCommon(cfg, n_streams, out);
+}
+
+gar_status gar_new_engine(double in_rate, double out_rate, int32_t preset, int32_t dtype, gar_resampler** out) {
+    if (!out) return guard(GAR_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    auto h = std::make_unique<gar_resampler>();
+    h->newPath = false;
+    h->channels = 1;
+    h->f64 = dtype != GAR_F32;
+    h->engineF32Io = dtype == GAR_F32;
+    if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
+    h->ratio = out_rate / in_rate;
+    return wrap([&]() -> gar_status {
+        gar_status st = initDevice(h.get());
+        if (st != GAR_OK) return st;
+        st = addStage(h.get(), in_rate, out_rate, presetToEngineQuality(preset));
+        if (st != GAR_OK) return st;
+        h->ratio = h->stages[0]->d.ratio;
+        h->groups.push_back(freshGroup(h.get(), 0, 1));
+        *out = h.release();
+        return GAR_OK;
+    });
+}
+
+gar_status gar_new_engine_dry(double in_rate, double out_rate, int32_t preset, int32_t dtype, gar_resampler** out) {
+    // Host-only engine (used by CPU tests of the stream-length state machine).
+    if (!out) return GAR_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto h = std::make_unique<gar_resampler>();
+    h->newPath = false;
+    h->dry = true;
+    h->f64 = dtype != GAR_F32;
+    if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
+    return wrap([&]() -> gar_status {
+        gar_status st = addStage(h.get(), in_rate, out_rate, presetToEngineQuality(preset));
+        if (st != GAR_OK) return st;
+        h->ratio = h->stages[0]->d.ratio;
+        h->groups.push_back(freshGroup(h.get(), 0, 1));
+        *out = h.release();
+        return GAR_OK;
+    });
+}
+
+void gar_free(gar_resampler* r) {
+    if (!r) return;
+    try {
+        if (r->stream) (void)hipStreamSynchronize(r->stream);
+        r->groups.clear();
+        r->stages.clear();
+        if (r->stream) (void)hipStreamDestroy(r->stream);
+    } catch (...) {
+    }
+    delete r;
+}
+
+int64_t gar_estimate_output(const gar_resampler* r, int64_t n) { return r ? estimate(r, n) : -1; }
+
+int64_t gar_output_size(const gar_resampler* r, int32_t ch, int64_t n) {
+    if (!r || ch < 0 || ch >= r->channels) return -1;
+    gar_resampler* h = const_cast<gar_resampler*>(r);
+    Group* g = groupOf(h, ch);
+    std::vector<int64_t> s;
+    return simulate(h, *g, n, false, s);
+}
+
+int64_t gar_flush_size(const gar_resampler* r, int32_t ch) {
+    if (!r || ch < 0 || ch >= r->channels) return -1;
+    gar_resampler* h = const_cast<gar_resampler*>(r);
+    Group* g = groupOf(h, ch);
+    std::vector<int64_t> s;
+    return simulate(h, *g, 0, true, s);
+}
+
+gar_status gar_process_f64(gar_resampler* r, const double* in, int64_t n, double* out, int64_t cap, int64_t* n_out) {
+    return monoCall<double>(r, 0, in, n, out, cap, n_out, false, false);
+}
+gar_status gar_process_f32(gar_resampler* r, const float* in, int64_t n, float* out, int64_t cap, int64_t* n_out) {
+    return monoCall<float>(r, 0, in, n, out, cap, n_out, false, false);
+}
+gar_status gar_process_into_f64(gar_resampler* r, const double* in, int64_t n, double* out, int64_t cap,
+                                int64_t* n_out) {
+    return monoCall<double>(r, 0, in, n, out, cap, n_out, false, true);
+}
+gar_status gar_process_into_f32(gar_resampler* r, const float* in, int64_t n, float* out, int64_t cap,
+                                int64_t* n_out) {
+    return monoCall<float>(r, 0, in, n, out, cap, n_out, false, true);
+}
+gar_status gar_flush_f64(gar_resampler* r, double* out, int64_t cap, int64_t* n_out) {
+    return monoCall<double>(r, 0, nullptr, 0, out, cap, n_out, true, false);
+}
+gar_status gar_flush_f32(gar_resampler* r, float* out, int64_t cap, int64_t* n_out) {
+    return monoCall<float>(r, 0, nullptr, 0, out, cap, n_out, true, false);
+}
+
+gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int32_t nch, int64_t n,
+                                 double* const* out, int64_t cap, int64_t* n_out) {
+    if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
+    if (nch != r->channels) {
+        g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(nch);
+        return GAR_ERR_CHANNEL_MISMATCH;
+    }
+    return wrap([&]() -> gar_status {
+        gar_resampler* h = r;
+        // exact sizes first: no state changes on BUFFER_TOO_SMALL
+        for (auto& g : h->groups) {
+            std::vector<int64_t> s;
+            if (simulate(h, g, n, false, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+        }
+        const int C = h->channels;
+        InView base;
+        base.n = n;
+        base.f64 = 1;
+        base.fs = 1;
+        base.cs = n;
+        if (!h->dry && n > 0) {
+            h->inStage.ensure(static_cast<size_t>(n) * C * 8);
+            for (int c = 0; c < C; ++c)
+                HIPCHK(hipMemcpyAsync(static_cast<char*>(h->inStage.p) + static_cast<size_t>(c) * n * 8, in[c], n * 8,
+                                      hipMemcpyHostToDevice, h->stream));
+        }
+        const int64_t ocap = std::max<int64_t>(cap, 1);
+        if (!h->dry) h->outStage.ensure(static_cast<size_t>(ocap) * C * 8);
+        for (auto& g : h->groups) {
+            InView iv = base;
+            if (!h->dry) iv.p = static_cast<const char*>(h->inStage.p) + static_cast<size_t>(g.c0) * n * 8;
+            OutView ov;
+            ov.f64 = 1;
+            ov.fs = 1;
+            ov.cs = ocap;
+            if (!h->dry) ov.p = static_cast<char*>(h->outStage.p) + static_cast<size_t>(g.c0) * ocap * 8;
+            gar_status st;
+            const int64_t got = runGroup(h, g, iv, ov, false, h->stream, cap, st);
+            if (st != GAR_OK) return st;
+            for (int c = g.c0; c < g.c0 + g.C; ++c) {
+                if (n_out) n_out[c] = got;
+                if (!h->dry && got > 0)
+                    HIPCHK(hipMemcpyAsync(out[c], static_cast<char*>(h->outStage.p) + static_cast<size_t>(c) * ocap * 8,
+                                          got * 8, hipMemcpyDeviceToHost, h->stream));
+            }
+        }
+        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        return GAR_OK;
+    });
+}
+
+gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch, int64_t cap, int64_t* n_out) {
+    if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
+    if (nch != r->channels) return guard(GAR_ERR_CHANNEL_MISMATCH, "channel count mismatch");
+    return wrap([&]() -> gar_status {
+        gar_resampler* h = r;
+        for (auto& g : h->groups) {
+            std::vector<int64_t> s;
+            if (simulate(h, g, 0, true, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+        }
+        const int C = h->channels;
+        const int64_t ocap = std::max<int64_t>(cap, 1);
+        if (!h->dry) h->outStage.ensure(static_cast<size_t>(ocap) * C * 8);
+        for (auto& g : h->groups) {
+            OutView ov;
+            ov.f64 = 1;
+            ov.fs = 1;
+            ov.cs = ocap;
+            if (!h->dry) ov.p = static_cast<char*>(h->outStage.p) + static_cast<size_t>(g.c0) * ocap * 8;
+            gar_status st;
+            const int64_t got = runGroup(h, g, InView(), ov, true, h->stream, cap, st);
+            if (st != GAR_OK) return st;
+            for (int c = g.c0; c < g.c0 + g.C; ++c) {
+                if (n_out) n_out[c] = got;
+                if (!h->dry && got > 0)
+                    HIPCHK(hipMemcpyAsync(out[c], static_cast<char*>(h->outStage.p) + static_cast<size_t>(c) * ocap * 8,
+                                          got * 8, hipMemcpyDeviceToHost, h->stream));
+            }
+        }
+        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        return GAR_OK;
+    });
+}
+
+int64_t gar_device_output_size(const gar_resampler* r, int64_t frames) {
+    if (!r || r->groups.size() != 1) return -1;
+    gar_resampler* h = const_cast<gar_resampler*>(r);
+    std::vector<int64_t> s;
+    return simulate(h, h->groups[0], frames, false, s);
+}
+
+int64_t gar_device_flush_size(const gar_resampler* r) {
+    if (!r || r->groups.size() != 1) return -1;
+    gar_resampler* h = const_cast<gar_resampler*>(r);
+    std::vector<int64_t> s;
+    return simulate(h, h->groups[0], 0, true, s);
+}
+
+gar_status gar_process_device(gar_resampler* r, const void* in, int32_t in_dtype, int64_t in_fs, int64_t in_cs,
+                              int64_t frames, void* out, int32_t out_dtype, int64_t out_fs, int64_t out_cs,
+                              int64_t out_cap, int64_t* out_frames, void* stream) {
+    if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
+    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep (per-channel calls were made)");
+    if (out_frames) *out_frames = 0;
+    return wrap([&]() -> gar_status {
+        InView iv;
+        iv.p = in;
+        iv.f64 = in_dtype == GAR_F64 ? 1 : 0;
+        iv.fs = in_fs;
+        iv.cs = in_cs;
+        iv.n = frames;
+        OutView ov;
+        ov.p = out;
+        ov.f64 = out_dtype == GAR_F64 ? 1 : 0;
+        ov.fs = out_fs;
+        ov.cs = out_cs;
+        gar_status st;
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+        const int64_t got = runGroup(r, r->groups[0], iv, ov, false, s, out_cap, st);
+        if (st == GAR_OK && out_frames) *out_frames = got;
+        return st;
+    });
+}
+
+gar_status gar_flush_device(gar_resampler* r, void* out, int32_t out_dtype, int64_t out_fs, int64_t out_cs,
+                            int64_t out_cap, int64_t* out_frames, void* stream) {
+    if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
+    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep");
+    if (out_frames) *out_frames = 0;
+    return wrap([&]() -> gar_status {
+        OutView ov;
+        ov.p = out;
+        ov.f64 = out_dtype == GAR_F64 ? 1 : 0;
+        ov.fs = out_fs;
+        ov.cs = out_cs;
+        gar_status st;
+        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+        const int64_t got = runGroup(r, r->groups[0], InView(), ov, true, s, out_cap, st);
+        if (st == GAR_OK && out_frames) *out_frames = got;
+        return st;
+    });
+}
+
+void gar_reset(gar_resampler* r) {
+    if (!r) return;
+    try {
+        if (r->stream) (void)hipStreamSynchronize(r->stream);
+        r->groups.clear();
+        r->groups.push_back(freshGroup(r, 0, r->channels));
+    } catch (...) {
+    }
+}
+
+double gar_get_ratio(const gar_resampler* r) { return r ? r->ratio : 0.0; }
+
+int32_t gar_get_latency(const gar_resampler* r) {
+    if (!r || r->stages.empty()) return 0;
+    int tot = 0;
+    for (const auto& s : r->stages) tot += static_cast<int>(static_cast<double>(stageLatency(s->d)) * s->d.ratio);
+    return tot;
+}
+
+int32_t gar_channels(const gar_resampler* r) { return r ? r->channels : 0; }
+
+gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
+    if (!r || !info) return GAR_ERR_INVALID_ARGUMENT;
+    std::memset(info, 0, sizeof(*info));
+    std::snprintf(info->algorithm, sizeof(info->algorithm), "%s", "multi-stage");
+    info->latency = gar_get_latency(r);
+    int64_t mem = 0;
+    for (const auto& s : r->stages)
+        mem += static_cast<int64_t>(s->fusedA.cap + s->dftA.cap + s->decimA.cap + s->pa.cap * 4);
+    for (const auto& g : r->groups)
+        for (const auto& d : g.dev) mem += static_cast<int64_t>(d.xh.buf[0].cap + d.xh.buf[1].cap + d.uh.buf[0].cap + d.uh.buf[1].cap);
+    info->memory_usage = mem;
+    if (!r->stages.empty()) {
+        const EngineDesign& d = r->stages[0]->d;
+        int len = 0;
+        if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1) len += d.dft.taps * d.dft.factor;
+        if (d.kind == EngineKind::DftPoly) len += d.poly.taps * d.poly.L;
+        info->filter_length = len;
+        info->phases = d.kind == EngineKind::DftPoly ? d.poly.L : 0;
+        info->simd_enabled = 1;
+        std::snprintf(info->simd_type, sizeof(info->simd_type), "%s", "gfx950 MFMA (HIP)");
+    }
+    return GAR_OK;
+}
+
+const char* gar_status_string(gar_status s) {
+    switch (s) {
+        case GAR_OK: return "ok";
+        case GAR_ERR_INVALID_CONFIG: return "invalid resampler configuration";
+        case GAR_ERR_BUFFER_TOO_SMALL: return "output buffer too small";
+        case GAR_ERR_NOT_SUPPORTED: return "operation not supported";
+        case GAR_ERR_CHANNEL_MISMATCH: return "channel count mismatch";
+        case GAR_ERR_DEVICE: return "device error";
+        case GAR_ERR_INTERNAL: return "internal error";
+        case GAR_ERR_INVALID_ARGUMENT: return "invalid argument";
+    }
+    return "unknown";
+}
+
+const char* gar_last_error(void) { return g_err.c_str(); }
+
+gar_status gar_design_engine(double in_rate, double out_rate, int32_t q, gar_engine_geometry* geom, double* dft,
+                             double* pa, double* pb, double* pc, double* pd, double* decim) {
+    EngineDesign d;
+    std::string err;
+    if (!designEngine(in_rate, out_rate, static_cast<Quality>(q), d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
+    if (geom) {
+        std::memset(geom, 0, sizeof(*geom));
+        geom->kind = static_cast<int32_t>(d.kind);
+        geom->dft_factor = d.dft.factor;
+        geom->dft_taps = d.dft.taps;
+        geom->poly_phases = d.poly.L;
+        geom->poly_taps = d.poly.taps;
+        geom->poly_step = d.poly.step;
+        geom->decim_factor = d.decim.factor;
+        geom->decim_taps = d.decim.taps;
+        FirPeriodic f;
+        bool have = false;
+        if (d.kind == EngineKind::DftPoly && firComposite(d.dft, d.poly, f)) { geom->fused = 1; have = true; }
+        else if (d.kind == EngineKind::DftOnly) { f = firFromDft(d.dft); have = true; }
+        else if (d.kind == EngineKind::Decim) { f = firFromDecim(d.decim); have = true; }
+        if (have) {
+            geom->fir_period_out = f.P;
+            geom->fir_period_in = f.Q;
+            for (const auto& row : f.rows) geom->fir_taps_max = std::max<int32_t>(geom->fir_taps_max, static_cast<int32_t>(row.size()));
+            BgPlan p;
+            if (buildBgPlan(f, false, p)) {
+                geom->useful_macs_per_output = p.usefulMacsPerOutput;
+                geom->mfma_macs_per_output = p.mfmaMacsPerOutput;
+            }
+        }
+    }
+    if (dft && !d.dft.c.empty()) std::memcpy(dft, d.dft.c.data(), d.dft.c.size() * 8);
+    if (pa && !d.poly.a.empty()) std::memcpy(pa, d.poly.a.data(), d.poly.a.size() * 8);
+    if (pb && !d.poly.b.empty()) std::memcpy(pb, d.poly.b.data(), d.poly.b.size() * 8);
+    if (pc && !d.poly.cc.empty()) std::memcpy(pc, d.poly.cc.data(), d.poly.cc.size() * 8);
+    if (pd && !d.poly.d.empty()) std::memcpy(pd, d.poly.d.data(), d.poly.d.size() * 8);
+    if (decim && !d.decim.c.empty()) std::memcpy(decim, d.decim.c.data(), d.decim.c.size() * 8);
+    return GAR_OK;
+}
+
+gar_status gar_design_composite(double in_rate, double out_rate, int32_t q, double* rows, int64_t* offsets) {
+    EngineDesign d;
+    std::string err;
+    if (!designEngine(in_rate, out_rate, static_cast<Quality>(q), d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
+    FirPeriodic f;
+    if (d.kind != EngineKind::DftPoly || !firComposite(d.dft, d.poly, f)) return guard(GAR_ERR_NOT_SUPPORTED, "no composite FIR");
+    size_t w = 0;
+    for (const auto& r : f.rows) w = std::max(w, r.size());
+    for (int r = 0; r < f.P; ++r) {
+        if (offsets) offsets[r] = f.off[r];
+        if (rows)
+            for (size_t k = 0; k < w; ++k) rows[r * w + k] = k < f.rows[r].size() ? f.rows[r][k] : 0.0;
+    }
+    return GAR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,59 @@
+// gar_kernels.hpp -- device-side descriptors and launchers (gar_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gar {
+
+// A channel group's input stream seen by a kernel: the retained history
+// (compute dtype, interleaved [t][C] with row stride hist_ld) virtually
+// concatenated with the caller's new input (any strides, f32 or f64), and
+// zero beyond valid_end -- the zero padding that DFTStage/PolyphaseStage/
+// DFTDecimationStage.Flush append (dft_stage.go:347, :582,
+// polyphase_stage.go:342) never has to be materialised.
+struct SrcDesc {
+    const void* hist;
+    int64_t hist_base, hist_len, hist_ld;
+    const void* in;
+    int64_t in_base, in_len, in_fs, in_cs;
+    int in_f64;
+    int64_t valid_end;
+};
+
+// Output view: element (o, c) -> out[(o - o0) * fs + c * cs]; only o in [o_lo, o_hi) written.
+struct OutDesc {
+    void* out;
+    int64_t o0, fs, cs;
+    int f64;
+    int64_t o_lo, o_hi;
+};
+
+// Device copy of a BgPlan (gar_plan.hpp).
+struct BgDev {
+    int f64;
+    int Pc, Qc, Kc, NS, nrb, ntasks, ksplit;
+    const void* A;      // [ntasks][NS][64]
+    const int* tasks;   // [ntasks][5] = rb, k0, ns, ks, nks
+};
+
+// General polyphase stage with live cubic coefficient interpolation
+// (polyphase_stage.go:257-293): output m uses at = at0 + m*step (local).
+struct PolyDev {
+    int f64;
+    int L, T;
+    int64_t step, at0, u_base;  // u_base = global stream index of local history index 0
+    const void *a, *b, *c, *d;  // [L][T] reversed, compute dtype
+};
+
+// Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
+hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
+                      hipStream_t stream);
+// dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.
+hipError_t launchGather(int f64, const SrcDesc& src, void* dst, int64_t t0, int64_t n, int C, hipStream_t stream);
+// Strided copy with dtype conversion (pass-through stages, group split).
+hipError_t launchCopy(const void* src, int src_f64, int64_t s_fs, int64_t s_cs, void* dst, int dst_f64,
+                      int64_t d_fs, int64_t d_cs, int64_t n, int C, hipStream_t stream);
+
+}  // namespace gar

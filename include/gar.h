@@ -1,0 +1,193 @@
+/*
+ * gar.h -- C ABI of the MI355X-native polyphase-FIR resampling engine.
+ *
+ * Drop-in boundary for tphakala/go-audio-resampler's resampling path: every
+ * entry point below replaces one Go entry point (cited path:line relative to
+ * the reference repo) and keeps its argument meaning, output lengths, state
+ * semantics and error behaviour.  A cgo shim implementing the Go
+ * `resampler.Resampler` interface over this ABI is given in INTEGRATION.md.
+ *
+ * Plain C types only: pointers, sizes, doubles.  Host-memory entry points
+ * (the cgo path) copy through the GPU; the *_device entry points take
+ * device-resident buffers and a HIP stream (hipStream_t passed as void*).
+ *
+ * Streams: interleaved multi-channel data uses element (t, c) at
+ * base[t * frame_stride + c * channel_stride]  (interleaved: (C, 1);
+ * planar with pitch P: (1, P)).
+ */
+#ifndef GAR_H
+#define GAR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gar_resampler gar_resampler;
+
+/* Status codes map 1:1 to the Go sentinels (resample.go:156-165). */
+typedef enum gar_status {
+    GAR_OK = 0,
+    GAR_ERR_INVALID_CONFIG = 1,   /* ErrInvalidConfig   resample.go:158 */
+    GAR_ERR_BUFFER_TOO_SMALL = 2, /* ErrBufferTooSmall  resample.go:161 -- returned before any state change */
+    GAR_ERR_NOT_SUPPORTED = 3,    /* ErrNotSupported    resample.go:164 */
+    GAR_ERR_CHANNEL_MISMATCH = 4, /* "expected %d channels, got %d" constant.go:205-207 */
+    GAR_ERR_DEVICE = 5,           /* HIP runtime failure / no MI355X visible */
+    GAR_ERR_INTERNAL = 6,         /* EstimateOutput underestimate (the Go code panics, constant.go:340-342) */
+    GAR_ERR_INVALID_ARGUMENT = 7  /* NULL handle / bad channel index ("channel %d out of range" constant.go:256) */
+} gar_status;
+
+/* resampler.QualityPreset (resample.go:104-131) */
+enum { GAR_QUALITY_QUICK = 0, GAR_QUALITY_LOW = 1, GAR_QUALITY_MEDIUM = 2, GAR_QUALITY_HIGH = 3,
+       GAR_QUALITY_VERYHIGH = 4, GAR_QUALITY_CUSTOM = 5 };
+/* resampler.QualityFlags (resample.go:133-153) */
+enum { GAR_FLAG_NO_INTERPOLATION = 1, GAR_FLAG_MINIMUM_PHASE = 2, GAR_FLAG_LINEAR_PHASE = 4,
+       GAR_FLAG_ALLOW_ALIASING = 8, GAR_FLAG_NO_SIMD = 16 };
+/* sample / compute types */
+enum { GAR_F64 = 0, GAR_F32 = 1 };
+/* engine.Quality (internal/engine/filter_params.go:16-41), for gar_design_engine */
+enum { GAR_ENGINE_QUICK = 0, GAR_ENGINE_LOW, GAR_ENGINE_MEDIUM, GAR_ENGINE_HIGH, GAR_ENGINE_VERYHIGH,
+       GAR_ENGINE_16BIT, GAR_ENGINE_20BIT, GAR_ENGINE_24BIT, GAR_ENGINE_28BIT, GAR_ENGINE_32BIT };
+
+/* resampler.QualitySpec (resample.go:77-102) */
+typedef struct gar_quality_spec {
+    int32_t preset;
+    int32_t precision;
+    double phase_response;
+    double passband_end;
+    double stopband_begin;
+    uint32_t flags;
+} gar_quality_spec;
+
+/* resampler.Config (resample.go:46-73) + three engine extensions. */
+typedef struct gar_config {
+    double input_rate;
+    double output_rate;
+    int32_t channels;
+    gar_quality_spec quality;
+    int64_t max_input_size;
+    int32_t enable_simd;
+    int32_t enable_parallel;
+    /* extensions (zero = reference behaviour) */
+    int32_t compute_dtype; /* GAR_F64 (the New path computes in float64, constant.go:121-146) or GAR_F32 */
+    int32_t device;        /* HIP device ordinal */
+    int32_t dry_run;       /* 1: host state machine only, no GPU work; process calls report lengths only */
+} gar_config;
+
+/* resampler.Info (resample.go:294-316) */
+typedef struct gar_info {
+    char algorithm[32];
+    int32_t filter_length;
+    int32_t phases;
+    int32_t latency;
+    int64_t memory_usage;
+    int32_t simd_enabled;
+    char simd_type[48];
+} gar_info;
+
+/* ---- construction -------------------------------------------------------- */
+/* Config.Validate (resample.go:168-214). */
+gar_status gar_config_validate(const gar_config *cfg);
+/* GetPresetSpec (resample.go:217-267). */
+gar_quality_spec gar_preset_spec(int32_t preset);
+/* resampler.New (resample.go:272-292).  Like the Go code, a non-custom preset
+ * is expanded into cfg->quality (resample.go:282-284). */
+gar_status gar_new(gar_config *cfg, gar_resampler **out);
+/* n_streams independent New(cfg) resamplers processed in lockstep as one GPU
+ * batch (channel index = stream * cfg->channels + ch).  Each stream obeys the
+ * reference's 256-channel limit (constants.go:9). */
+gar_status gar_new_batch(gar_config *cfg, int32_t n_streams, gar_resampler **out);
+/* resampler.NewEngine (convenience.go:125) when dtype == GAR_F64,
+ * resampler.NewEngineFloat32 (convenience.go:329) when dtype == GAR_F32. */
+gar_status gar_new_engine(double input_rate, double output_rate, int32_t preset, int32_t dtype,
+                          gar_resampler **out);
+void gar_free(gar_resampler *r);
+/* Host-only NewEngine (no GPU work; process calls report exact lengths only).
+ * Used to test the stream-length state machine on machines without a GPU. */
+gar_status gar_new_engine_dry(double input_rate, double output_rate, int32_t preset, int32_t dtype,
+                              gar_resampler **out);
+
+/* ---- host-memory streaming (cgo path; channel 0 unless noted) ------------- */
+/* EstimateOutput (constant.go:117-119, convenience.go:168-170). */
+int64_t gar_estimate_output(const gar_resampler *r, int64_t input_len);
+/* Exact number of samples the next process call on `channel` would return. */
+int64_t gar_output_size(const gar_resampler *r, int32_t channel, int64_t input_len);
+/* Exact number of samples Flush on `channel` would return now. */
+int64_t gar_flush_size(const gar_resampler *r, int32_t channel);
+
+/* Process / ProcessFloat32 (constant.go:88-146, convenience.go:138,341): fills
+ * out[0:*n_out]; GAR_ERR_BUFFER_TOO_SMALL (no state change) if cap < the exact
+ * output size. */
+gar_status gar_process_f64(gar_resampler *r, const double *in, int64_t n, double *out, int64_t cap, int64_t *n_out);
+gar_status gar_process_f32(gar_resampler *r, const float *in, int64_t n, float *out, int64_t cap, int64_t *n_out);
+/* ProcessInto / ProcessFloat32Into (constant.go:103-112, :161-199,
+ * convenience.go:145-160, :351-366): GAR_ERR_BUFFER_TOO_SMALL before any state
+ * change when cap < EstimateOutput(n). */
+gar_status gar_process_into_f64(gar_resampler *r, const double *in, int64_t n, double *out, int64_t cap,
+                                int64_t *n_out);
+gar_status gar_process_into_f32(gar_resampler *r, const float *in, int64_t n, float *out, int64_t cap,
+                                int64_t *n_out);
+/* ProcessMulti (constant.go:204-252): in[c][0:n] planar; out[c] with capacity
+ * cap each; n_out[c] per channel. */
+gar_status gar_process_multi_f64(gar_resampler *r, const double *const *in, int32_t n_channels, int64_t n,
+                                 double *const *out, int64_t cap, int64_t *n_out);
+/* Flush (constant.go:349-354, resampler.go:275-322): channel 0. */
+gar_status gar_flush_f64(gar_resampler *r, double *out, int64_t cap, int64_t *n_out);
+gar_status gar_flush_f32(gar_resampler *r, float *out, int64_t cap, int64_t *n_out);
+/* FlushMulti (constant.go:390-404). */
+gar_status gar_flush_multi_f64(gar_resampler *r, double *const *out, int32_t n_channels, int64_t cap,
+                               int64_t *n_out);
+
+/* ---- device-resident batched streaming (all channels in lockstep) -------- */
+/* Process `frames` frames of all channels from device memory `in` (dtype
+ * in_dtype) into device memory `out`; *out_frames = frames produced per
+ * channel.  GAR_ERR_BUFFER_TOO_SMALL (no state change) if out_cap_frames is
+ * smaller than the exact output size.  Asynchronous on `stream` (NULL = the
+ * handle's own stream); returns once the work is enqueued. */
+gar_status gar_process_device(gar_resampler *r, const void *in, int32_t in_dtype, int64_t in_frame_stride,
+                              int64_t in_channel_stride, int64_t frames, void *out, int32_t out_dtype,
+                              int64_t out_frame_stride, int64_t out_channel_stride, int64_t out_cap_frames,
+                              int64_t *out_frames, void *stream);
+/* Flush all channels into device memory (FlushMulti semantics). */
+gar_status gar_flush_device(gar_resampler *r, void *out, int32_t out_dtype, int64_t out_frame_stride,
+                            int64_t out_channel_stride, int64_t out_cap_frames, int64_t *out_frames, void *stream);
+/* Exact lockstep output sizes (-1 if channels are not in lockstep). */
+int64_t gar_device_output_size(const gar_resampler *r, int64_t frames);
+int64_t gar_device_flush_size(const gar_resampler *r);
+
+/* ---- state / introspection ----------------------------------------------- */
+void gar_reset(gar_resampler *r);                       /* Reset (constant.go:429-444, resampler.go:325-340) */
+double gar_get_ratio(const gar_resampler *r);           /* GetRatio (constant.go:447) */
+int32_t gar_get_latency(const gar_resampler *r);        /* GetLatency (constant.go:407-426) */
+gar_status gar_get_info(const gar_resampler *r, gar_info *info); /* GetInfo (constant.go:452-485) */
+int32_t gar_channels(const gar_resampler *r);
+const char *gar_status_string(gar_status s);
+const char *gar_last_error(void);                       /* thread-local detail for the last failure */
+
+/* ---- host-only design introspection (no GPU needed) ----------------------- */
+typedef struct gar_engine_geometry {
+    int32_t kind; /* 0 cubic, 1 DFT-only, 2 DFT x2 + polyphase, 3 decimator, 4 pass-through */
+    int32_t dft_factor, dft_taps;
+    int32_t poly_phases, poly_taps;
+    int64_t poly_step;
+    int32_t decim_factor, decim_taps;
+    int32_t fused;                 /* DFT+polyphase composed into one MFMA FIR (step has no fraction) */
+    int32_t fir_period_out, fir_period_in, fir_taps_max;
+    double useful_macs_per_output; /* of the MFMA FIR executed for this engine */
+    double mfma_macs_per_output;
+} gar_engine_geometry;
+/* engine.NewResampler[float64](in, out, quality) design (resampler.go:51-179).
+ * Any output buffer may be NULL: dft [factor*taps], poly_* [phases*taps] (the
+ * Go layout), decim [taps]. */
+gar_status gar_design_engine(double input_rate, double output_rate, int32_t engine_quality,
+                             gar_engine_geometry *geom, double *dft, double *poly_a, double *poly_b,
+                             double *poly_c, double *poly_d, double *decim);
+/* Composite FIR of a fused DFT+polyphase engine: rows [P][taps_max] (zero padded), offsets [P]. */
+gar_status gar_design_composite(double input_rate, double output_rate, int32_t engine_quality, double *rows,
+                                int64_t *offsets);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GAR_H */
