@@ -272,6 +272,12 @@ struct gar_resampler {
     std::vector<gar::Group> groups;
     gar::DevBuf inStage, outStage;
     std::vector<int64_t> scratchSizes;
+    // optional HIP-event timing of the MFMA FIR launches (bench.py roofline)
+    bool profile = false;
+    struct Ev { int tag; hipEvent_t a, b; };
+    std::vector<Ev> events;
+    double profiledMs[3] = {0, 0, 0};
+    int64_t profiledLaunches[3] = {0, 0, 0};
 };
 
 namespace gar {
@@ -285,6 +291,19 @@ struct Ctx {
     hipStream_t s;
     bool launch;
 };
+
+// launchBg bracketed by HIP events on the launch stream when profiling is on.
+hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
+    if (!x.h->profile) return launchBg(p, src, od, C, x.s);
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, x.s));
+    const hipError_t e = launchBg(p, src, od, C, x.s);
+    HIPCHK(hipEventRecord(b, x.s));
+    x.h->events.push_back({tag, a, b});
+    return e;
+}
 
 SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
     SrcDesc s{};
@@ -338,7 +357,7 @@ void materialize(Ctx& x, StageRT& rt, Counters& c, StageDev& dv, const SrcDesc& 
         const int64_t n = c.u_count - c.u_base;
         uh.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(n, 1)) * C * tc);
         OutView ov{uh.buf[other].p, C, 1, rt.f64 ? 1 : 0};
-        HIPCHK(launchBg(rt.dftD, xsrc, mkOut(ov, c.u_base, n), C, x.s));
+        HIPCHK(timedBg(x, 1, rt.dftD, xsrc, mkOut(ov, c.u_base, n), C));
         uh.cur = other;
         uh.base = c.u_base;
         uh.len = n;
@@ -371,7 +390,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t y0 = c.y_count;
             const int64_t nout = cntDft(c, d.dft, n);
             const SrcDesc src = mkSrc(dv.xh, C, x0, in);
-            if (x.launch && nout > 0) HIPCHK(launchBg(rt.dftD, src, mkOut(out, y0, nout), C, x.s));
+            if (x.launch && nout > 0) HIPCHK(timedBg(x, 1, rt.dftD, src, mkOut(out, y0, nout), C));
             hist_update(x, dv.xh, src, c.x_count - c.dft_hist, c.x_count);
             c.y_count += nout;
             return nout;
@@ -381,7 +400,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t y0 = c.y_count;
             const int64_t nout = cntDecim(c, d.decim, n);
             const SrcDesc src = mkSrc(dv.xh, C, x0, in);
-            if (x.launch && nout > 0) HIPCHK(launchBg(rt.decimD, src, mkOut(out, y0, nout), C, x.s));
+            if (x.launch && nout > 0) HIPCHK(timedBg(x, 2, rt.decimD, src, mkOut(out, y0, nout), C));
             hist_update(x, dv.xh, src, c.x_count - c.dec_hist, c.x_count);
             c.y_count += nout;
             return nout;
@@ -396,7 +415,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t nout = cntPoly(c, d.poly, nu, quirk);
             if (!c.staged) {
                 // Fused: DFT x2 and polyphase composed into one MFMA FIR over x.
-                if (x.launch && nout > 0) HIPCHK(launchBg(rt.fusedD, xsrc, mkOut(out, y0, nout), C, x.s));
+                if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C));
                 if (quirk) {
                     materialize(x, rt, c, dv, xsrc);
                 } else {
@@ -411,7 +430,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                     x.g->utmp.ensure(static_cast<size_t>(std::max<int64_t>(nu, 1)) * C * rt.tc());
                     if (nu > 0) {
                         OutView uv{x.g->utmp.p, C, 1, rt.f64 ? 1 : 0};
-                        HIPCHK(launchBg(rt.dftD, xsrc, mkOut(uv, dy0, nu), C, x.s));
+                        HIPCHK(timedBg(x, 1, rt.dftD, xsrc, mkOut(uv, dy0, nu), C));
                     }
                 }
                 uin.p = x.g->utmp.p; uin.fs = C; uin.cs = 1; uin.f64 = rt.f64 ? 1 : 0; uin.n = nu;
@@ -1051,7 +1070,7 @@ gar_status gar_process_device(gar_resampler* r, const void* in, int32_t in_dtype
         ov.fs = out_fs;
         ov.cs = out_cs;
         gar_status st;
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
         const int64_t got = runGroup(r, r->groups[0], iv, ov, false, s, out_cap, st);
         if (st == GAR_OK && out_frames) *out_frames = got;
         return st;
@@ -1070,7 +1089,7 @@ gar_status gar_flush_device(gar_resampler* r, void* out, int32_t out_dtype, int6
         ov.fs = out_fs;
         ov.cs = out_cs;
         gar_status st;
-        hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->stream;
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
         const int64_t got = runGroup(r, r->groups[0], InView(), ov, true, s, out_cap, st);
         if (st == GAR_OK && out_frames) *out_frames = got;
         return st;
@@ -1137,6 +1156,32 @@ const char* gar_status_string(gar_status s) {
 }
 
 const char* gar_last_error(void) { return g_err.c_str(); }
+
+void gar_profile_enable(gar_resampler* r, int32_t on) {
+    if (!r) return;
+    r->profile = on != 0;
+}
+
+gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t* launches) {
+    if (!r || kind < 0 || kind > 2) return GAR_ERR_INVALID_ARGUMENT;
+    return wrap([&]() -> gar_status {
+        for (auto& ev : r->events) {
+            HIPCHK(hipEventSynchronize(ev.b));
+            float t = 0;
+            HIPCHK(hipEventElapsedTime(&t, ev.a, ev.b));
+            r->profiledMs[ev.tag] += t;
+            r->profiledLaunches[ev.tag] += 1;
+            (void)hipEventDestroy(ev.a);
+            (void)hipEventDestroy(ev.b);
+        }
+        r->events.clear();
+        if (ms) *ms = r->profiledMs[kind];
+        if (launches) *launches = r->profiledLaunches[kind];
+        r->profiledMs[kind] = 0;
+        r->profiledLaunches[kind] = 0;
+        return GAR_OK;
+    });
+}
 
 gar_status gar_design_engine(double in_rate, double out_rate, int32_t q, gar_engine_geometry* geom, double* dft,
                              double* pa, double* pb, double* pc, double* pd, double* decim) {

@@ -134,7 +134,7 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     plan.Pc = f.P * bestMp;
     plan.Qc = f.Q * bestMp;
     plan.nrb = static_cast<int>(rbs.size());
-    const int maxNS = f64 ? 64 : 128;
+    const int maxNS = f64 ? 48 : 112;
     int needNS = 0;
     for (int rb = 0; rb < plan.nrb; ++rb) {
         const int nst = rbs[rb].nsteps;
@@ -153,12 +153,10 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
         if (nks > 1) plan.ksplit = true;
         plan.Kc = std::max(plan.Kc, rbs[rb].klo + 4 * nst);
     }
-    static const int buckets32[] = {16, 32, 48, 64, 80, 96, 112, 128};
-    static const int buckets64[] = {16, 32, 48, 64};
-    plan.NS = 0;
-    if (f64) { for (int b : buckets64) if (b >= needNS) { plan.NS = b; break; } }
-    else { for (int b : buckets32) if (b >= needNS) { plan.NS = b; break; } }
-    if (plan.NS == 0) return false;
+    // Kernel instantiations exist for NS = 8, 12, ..., maxNS; the A image is
+    // zero padded to NS steps so the MFMA loop has no per-step guard.
+    plan.NS = std::max(8, (needNS + 3) / 4 * 4);
+    if (plan.NS > maxNS) return false;
 
     const size_t nt = plan.tasks.size();
     const size_t img = nt * plan.NS * 64;

@@ -88,7 +88,8 @@ EXPORTED = [
     "gar_process_into_f64", "gar_process_into_f32", "gar_process_multi_f64", "gar_flush_f64", "gar_flush_f32",
     "gar_flush_multi_f64", "gar_process_device", "gar_flush_device", "gar_device_output_size",
     "gar_device_flush_size", "gar_reset", "gar_get_ratio", "gar_get_latency", "gar_get_info", "gar_channels",
-    "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite",
+    "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite", "gar_profile_enable",
+    "gar_profile_read",
 ]
 
 _lib = None
@@ -135,6 +136,8 @@ def lib():
         "gar_last_error": (C.c_char_p, []),
         "gar_design_engine": (i32, [d, d, i32, C.POINTER(EngineGeometry), vp, vp, vp, vp, vp, vp]),
         "gar_design_composite": (i32, [d, d, i32, vp, vp]),
+        "gar_profile_enable": (None, [vp, i32]),
+        "gar_profile_read": (i32, [vp, i32, C.POINTER(d), C.POINTER(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -270,6 +273,15 @@ class Resampler:
         info = Info()
         _check(lib().gar_get_info(self._h, C.byref(info)))
         return info
+
+    def profile(self, on=True):
+        lib().gar_profile_enable(self._h, int(on))
+
+    def profile_read(self, kind=0):
+        """(total ms, launches) of one MFMA FIR kind (0 fused, 1 DFT, 2 decimator) since the last read."""
+        ms, n = C.c_double(0), C.c_int64(0)
+        _check(lib().gar_profile_read(self._h, kind, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
 
     @property
     def Channels(self):

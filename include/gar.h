@@ -144,7 +144,7 @@ gar_status gar_flush_multi_f64(gar_resampler *r, double *const *out, int32_t n_c
  * in_dtype) into device memory `out`; *out_frames = frames produced per
  * channel.  GAR_ERR_BUFFER_TOO_SMALL (no state change) if out_cap_frames is
  * smaller than the exact output size.  Asynchronous on `stream` (NULL = the
- * handle's own stream); returns once the work is enqueued. */
+ * default stream); returns once the work is enqueued. */
 gar_status gar_process_device(gar_resampler *r, const void *in, int32_t in_dtype, int64_t in_frame_stride,
                               int64_t in_channel_stride, int64_t frames, void *out, int32_t out_dtype,
                               int64_t out_frame_stride, int64_t out_channel_stride, int64_t out_cap_frames,
@@ -164,6 +164,11 @@ gar_status gar_get_info(const gar_resampler *r, gar_info *info); /* GetInfo (con
 int32_t gar_channels(const gar_resampler *r);
 const char *gar_status_string(gar_status s);
 const char *gar_last_error(void);                       /* thread-local detail for the last failure */
+/* HIP-event timing of every MFMA FIR launch (bracketed on its own stream). */
+void gar_profile_enable(gar_resampler *r, int32_t on);
+/* Sum of launch durations (ms) and launch count of one kernel kind (0 fused
+ * DFT+polyphase FIR, 1 DFT FIR, 2 decimator FIR) since its last read. */
+gar_status gar_profile_read(gar_resampler *r, int32_t kind, double *ms, int64_t *launches);
 
 /* ---- host-only design introspection (no GPU needed) ----------------------- */
 typedef struct gar_engine_geometry {
