@@ -16,7 +16,7 @@ template <class TC>
 __device__ __forceinline__ TC srcRead(const SrcDesc& s, int64_t t, int c) {
     if (t < 0 || t >= s.valid_end) return TC(0);
     const int64_t h = t - s.hist_base;
-    if (h >= 0 && h < s.hist_len) return static_cast<const TC*>(s.hist)[h * s.hist_ld + c];
+    if (h >= 0 && h < s.hist_len) return s.hist ? static_cast<const TC*>(s.hist)[h * s.hist_ld + c] : TC(0);
     const int64_t i = t - s.in_base;
     if (i >= 0 && i < s.in_len) {
         const int64_t e = i * s.in_fs + static_cast<int64_t>(c) * s.in_cs;

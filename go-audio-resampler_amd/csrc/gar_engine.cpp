@@ -224,8 +224,9 @@ struct Hist {
     DevBuf buf[2];
     int cur = 0;
     int64_t base = 0, len = 0;
-    void* ptr() const { return buf[cur].p; }
-    void clear() { base = 0; len = 0; }
+    bool zero = false;  // rows known to be all zero (post-flush state); nothing stored
+    void* ptr() const { return zero ? nullptr : buf[cur].p; }
+    void clear() { base = 0; len = 0; zero = false; }
 };
 
 struct StageDev {
@@ -337,13 +338,14 @@ void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
     const int C = x.g->C;
     const int tc = x.h->f64 ? 8 : 4;
     if (k1 < k0) k1 = k0;
-    if (!x.launch) { hs.base = k0; hs.len = k1 - k0; return; }
+    if (!x.launch) { hs.base = k0; hs.len = k1 - k0; hs.zero = false; return; }
     const int other = 1 - hs.cur;
     hs.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(k1 - k0, 1)) * C * tc);
     HIPCHK(launchGather(x.h->f64, src, hs.buf[other].p, k0, k1 - k0, C, x.s));
     hs.cur = other;
     hs.base = k0;
     hs.len = k1 - k0;
+    hs.zero = false;
 }
 
 // FUSED -> STAGED: rebuild the poly-stream history u[u_base, u_count) from x by
@@ -477,6 +479,29 @@ int64_t stageFlush(Ctx& x, int si, const OutView& out) {
                 InView none;
                 none.zeros = true;
                 const SrcDesc xsrc = mkSrc(dv.xh, C, c.x_count, none);
+                // Fused flush: DFTStage.Flush + PolyphaseStage.Process + PolyphaseStage.Flush
+                // counted exactly, all samples by one composite launch over x zero-extended
+                // (the zero pads of both flushes are zero samples of the same composite FIR).
+                Counters t = c;
+                bool quirk = false;
+                int64_t nA = 0, nB = 0;
+                if (t.dft_hist > 0) nA = cntPoly(t, d.poly, cntDft(t, d.dft, d.dft.taps), quirk);
+                if (t.poly_hist > 0) nB = cntPoly(t, d.poly, d.poly.taps, quirk);
+                if (!quirk) {
+                    const int64_t y0 = c.y_count, n = nA + nB;
+                    if (x.launch && n > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, n), C));
+                    c = t;
+                    c.y_count = y0 + n;
+                    c.staged = true;
+                    // both delay lines now hold only flush zeros (their last T-1 pad samples)
+                    dv.xh.base = c.x_count - c.dft_hist;
+                    dv.xh.len = c.dft_hist;
+                    dv.xh.zero = true;
+                    dv.uh.base = c.u_base;
+                    dv.uh.len = c.u_count - c.u_base;
+                    dv.uh.zero = true;
+                    return n;
+                }
                 materialize(x, rt, c, dv, xsrc);
             }
             int64_t total = 0;
@@ -608,7 +633,8 @@ Group splitCopy(Handle* h, Group& g, int k0, int kc) {
         for (int k = 0; k < 2; ++k) {
             dst[k]->base = src[k]->base;
             dst[k]->len = src[k]->len;
-            if (!h->dry && src[k]->len > 0) {
+            dst[k]->zero = src[k]->zero;
+            if (!h->dry && src[k]->len > 0 && !src[k]->zero) {
                 dst[k]->buf[0].ensure(static_cast<size_t>(src[k]->len) * kc * tc);
                 const char* sp = static_cast<const char*>(src[k]->ptr()) + static_cast<size_t>(k0) * tc;
                 HIPCHK(launchCopy(sp, h->f64, g.C, 1, dst[k]->buf[0].p, h->f64, kc, 1, src[k]->len, kc, h->stream));

@@ -656,3 +656,16 @@ API void o_new_stage_info(o_new_rs *r, int j, o_engine_info *inf) {
     if (s->is_cubic) { inf->kind = 0; return; }
     resampler_info_d(s->eng, inf);
 }
+
+/* ------------------------------------------------------------------------- */
+/* simdops primitive stand-ins exported for the KAT tests                     */
+/* (internal/simdops/ops_test.go:25-70)                                      */
+/* ------------------------------------------------------------------------- */
+API double o_dot(const double *a, const double *b, int64_t n) { return dot_d(a, b, n); }
+API void o_convolve_valid(double *dst, const double *sig, int64_t nsig, const double *ker, int64_t nker) {
+    convolve_valid_d(dst, sig, nsig, ker, nker);
+}
+API double o_cubic_interp_dot(const double *h, const double *a, const double *b, const double *c, const double *d,
+                              double x, int64_t n) {
+    return cubic_interp_dot_d(h, a, b, c, d, x, n);
+}

@@ -69,6 +69,8 @@ def lib():
             "o_new_reset": (None, [vp]), "o_new_latency": (i, [vp]), "o_new_estimate_output": (i64, [vp, i64]),
             "o_new_ratio": (d, [vp]), "o_new_nstages": (i, [vp, vp, vp]),
             "o_new_stage_info": (None, [vp, i, C.POINTER(EngineInfo)]),
+            "o_dot": (d, [vp, vp, i64]), "o_convolve_valid": (None, [vp, vp, i64, vp, i64]),
+            "o_cubic_interp_dot": (d, [vp, vp, vp, vp, vp, d, i64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -108,6 +110,23 @@ def design_lowpass_auto(fc, tbw, att, gain=1.0):
     if rc != 0:
         raise ValueError("invalid filter params")
     return out[: n.value].copy()
+
+
+def dot(a, b):
+    a, b = np.ascontiguousarray(a, float), np.ascontiguousarray(b, float)
+    return lib().o_dot(_ptr(a), _ptr(b), len(a))
+
+
+def convolve_valid(sig, ker):
+    sig, ker = np.ascontiguousarray(sig, float), np.ascontiguousarray(ker, float)
+    dst = np.zeros(max(len(sig) - len(ker) + 1, 0))
+    lib().o_convolve_valid(_ptr(dst), _ptr(sig), len(sig), _ptr(ker), len(ker))
+    return dst
+
+
+def cubic_interp_dot(h, a, b, c, d, x):
+    arrs = [np.ascontiguousarray(v, float) for v in (h, a, b, c, d)]
+    return lib().o_cubic_interp_dot(*[_ptr(v) for v in arrs], float(x), len(arrs[0]))
 
 
 def find_rational_approx(ratio):

@@ -1,0 +1,182 @@
+"""C-ABI boundary and host state machine, CPU only (dry-run handles do the
+reference's exact integer bookkeeping without touching a GPU)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import chunk_sizes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    hdr = open(os.path.join(ROOT, "include", "gar.h")).read()
+    return set(re.findall(r"^\s*(?:gar_status|void|int64_t|int32_t|double|const char \*|gar_quality_spec)\s+\**"
+                          r"(gar_\w+)\s*\(", hdr, re.M))
+
+
+def test_library_exports_every_declared_symbol(gar):
+    decl = header_symbols()
+    assert len(decl) >= 30
+    out = subprocess.run(["nm", "-D", "--defined-only", gar.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines()}
+    assert decl <= syms, decl - syms
+    assert set(gar.EXPORTED) <= syms
+    # code object for gfx950 is embedded
+    assert b"gfx950" in open(gar.LIB_PATH, "rb").read()
+
+
+def _validate(gar, **kw):
+    cfg = gar.Config(**kw)
+    return gar.lib().gar_config_validate(C.byref(cfg))
+
+
+def test_config_validate(gar):  # resample.go:168-214
+    ok = dict(InputRate=44100, OutputRate=48000, Channels=2)
+    assert _validate(gar, **ok) == 0
+    assert _validate(gar, **dict(ok, InputRate=0)) == gar.INVALID_CONFIG
+    assert _validate(gar, **dict(ok, OutputRate=-1)) == gar.INVALID_CONFIG
+    assert _validate(gar, **dict(ok, Channels=0)) == gar.INVALID_CONFIG
+    assert _validate(gar, **dict(ok, Channels=257)) == gar.INVALID_CONFIG
+    assert _validate(gar, **dict(ok, Channels=256)) == 0
+    assert _validate(gar, **dict(ok, OutputRate=44100 * 257)) == gar.INVALID_CONFIG
+    assert _validate(gar, **dict(ok, OutputRate=44100 / 257)) == gar.INVALID_CONFIG
+    bad = gar.QualitySpec(Preset=gar.QualityCustom, Precision=7, PhaseResponse=50, PassbandEnd=0.9, StopbandBegin=0.95)
+    assert _validate(gar, **dict(ok, Quality=bad)) == gar.INVALID_CONFIG
+    good = gar.QualitySpec(Preset=gar.QualityCustom, Precision=20, PhaseResponse=50, PassbandEnd=0.9, StopbandBegin=0.95)
+    assert _validate(gar, **dict(ok, Quality=good)) == 0
+    for field, val in (("PhaseResponse", 101), ("PassbandEnd", 1.0), ("StopbandBegin", 0.5)):
+        q = gar.QualitySpec(Preset=gar.QualityCustom, Precision=20, PhaseResponse=50, PassbandEnd=0.9, StopbandBegin=0.95)
+        setattr(q, field, val)
+        assert _validate(gar, **dict(ok, Quality=q)) == gar.INVALID_CONFIG
+    with pytest.raises(gar.ErrInvalidConfig):
+        gar.New(gar.Config(0, 48000, DryRun=True))
+
+
+def test_preset_specs(gar):  # resample.go:217-267
+    want = {0: (8, 0.7, 1.0), 1: (16, 0.80, 0.95), 2: (16, 0.90, 0.98), 3: (24, 0.95, 0.99), 4: (32, 0.99, 0.995)}
+    for p, (prec, pb, sb) in want.items():
+        s = gar.GetPresetSpec(p)
+        assert (s.Preset, s.Precision, s.PassbandEnd, s.StopbandBegin, s.PhaseResponse) == (p, prec, pb, sb, 50.0)
+
+
+def test_new_expands_preset_into_config(gar):  # resample.go:282-284 mutates the caller's config
+    cfg = gar.Config(44100, 48000, 1, gar.QualityVeryHigh, DryRun=True)
+    h = C.c_void_p(0)
+    assert gar.lib().gar_new(C.byref(cfg), C.byref(h)) == 0
+    assert cfg.Quality.Precision == 32 and abs(cfg.Quality.StopbandBegin - 0.995) < 1e-12
+    gar.lib().gar_free(h)
+
+
+def test_quick_preset_not_supported_yet(gar):
+    with pytest.raises(gar.ErrNotSupported):
+        gar.New(gar.Config(44100, 48000, 1, gar.QualityQuick, DryRun=True))
+
+
+ENGINE_PAIRS = [(44100, 48000), (48000, 44100), (48000, 96000), (96000, 48000), (48000, 16000), (16000, 44100),
+                (22050, 16000), (44100, 32000), (8000, 48000), (44100, 44100), (48000, 200), (1000, 255000)]
+
+
+@pytest.mark.parametrize("i,o", ENGINE_PAIRS)
+@pytest.mark.parametrize("preset", [1, 2, 3])
+def test_engine_stream_lengths(gar, O, i, o, preset):
+    """Every call returns exactly the reference's sample count: chunked Process,
+    Flush, Process after Flush without Reset, repeated Flush, Reset."""
+    rng = np.random.default_rng(0)
+    e = O.Engine(i, o, O.lib().o_preset_to_engine_quality(preset))
+    r = gar.NewEngineDry(i, o, preset)
+    for step in ([1, 5, 100, 4096, 3, 20000, 0, 1], ["f", 777, "f", "f", 31, "reset", 5000, "f"]):
+        for n in step:
+            if n == "f":
+                a, b = len(e.flush()), r.FlushSize()
+                r.Flush()
+            elif n == "reset":
+                e.reset(), r.Reset()
+                continue
+            else:
+                x = rng.standard_normal(n)
+                a, b = len(e.process(x)), r.OutputSize(n)
+                r.Process(x)
+            assert a == b, (n, a, b)
+
+
+NEW_PAIRS = [(44100, 48000), (48000, 44100), (96000, 44100), (96000, 16000), (192000, 48000), (48000, 8000),
+             (88200, 16000), (44100, 44200), (16000, 48000), (8000, 96000)]
+
+
+@pytest.mark.parametrize("i,o", NEW_PAIRS)
+@pytest.mark.parametrize("preset", [1, 2, 3, 4])
+def test_new_path_stream_lengths(gar, O, i, o, preset):
+    rng = np.random.default_rng(1)
+    ref = O.NewResampler(i, o, 1, preset)
+    g = gar.New(gar.Config(i, o, 1, preset, DryRun=True))
+    for n in chunk_sizes(30017, 4800) + [0, 17]:
+        x = rng.standard_normal(n)
+        assert len(ref.process(x)) == g.OutputSize(n)
+        g.Process(x)
+    assert len(ref.flush()) == g.FlushSize()
+    g.Flush()
+    x = rng.standard_normal(999)
+    assert len(ref.process(x)) == g.OutputSize(999)
+    assert g.GetLatency() == ref.latency()
+    assert g.GetRatio() == ref.ratio
+
+
+@pytest.mark.parametrize("i,o,preset", [(44100, 48000, 3), (48000, 44100, 4), (96000, 44100, 4), (48000, 16000, 1)])
+def test_estimate_output_is_upper_bound(gar, i, o, preset):  # processinto_test.go:311-453
+    g = gar.New(gar.Config(i, o, 1, preset, DryRun=True))
+    for n in [1, 7, 64, 1000, 4096, 4800, 48000] * 3:
+        assert g.OutputSize(n) <= g.EstimateOutput(n)
+        g.Process(np.zeros(n))
+        assert g.EstimateOutput(n) == int(n * (o / i)) + 64
+
+
+def test_buffer_too_small_does_not_advance_state(gar):  # processinto_test.go:176-227
+    g = gar.New(gar.Config(44100, 48000, 1, gar.QualityHigh, DryRun=True))
+    x = np.zeros(4096)
+    g.Process(x)
+    before = g.OutputSize(4096)
+    small = np.zeros(g.EstimateOutput(4096) - 1)
+    with pytest.raises(gar.ErrBufferTooSmall):
+        g.ProcessInto(x, small)
+    assert g.OutputSize(4096) == before
+    with pytest.raises(gar.ErrBufferTooSmall):
+        g.ProcessFloat32Into(x.astype(np.float32), np.zeros(len(small), np.float32))
+    assert g.OutputSize(4096) == before
+
+
+def test_channel_state_independence(gar, O):
+    """Process (channel 0 only, constant.go:88-95) advances channel 0 alone;
+    ProcessMulti then yields per-channel lengths exactly like the reference."""
+    rng = np.random.default_rng(2)
+    ref = O.NewResampler(48000, 44100, 3, O.P_HIGH)
+    g = gar.New(gar.Config(48000, 44100, 3, gar.QualityHigh, DryRun=True))
+    x0 = rng.standard_normal(1234)
+    ref.process(x0, 0)
+    g.Process(x0)
+    xs = [rng.standard_normal(5000) for _ in range(3)]
+    want = [len(ref.process(x, c)) for c, x in enumerate(xs)]
+    got = [g.OutputSize(5000, c) for c in range(3)]
+    assert got == want and got[0] != got[1]
+    with pytest.raises(gar.ErrChannelMismatch):
+        g.ProcessMulti(xs[:2])
+
+
+def test_latency_and_info(gar, O):  # constant.go:407-485
+    for (i, o, p) in [(44100, 48000, 3), (48000, 44100, 4), (96000, 44100, 4), (96000, 16000, 3)]:
+        g = gar.New(gar.Config(i, o, 2, p, DryRun=True))
+        assert g.GetLatency() == O.NewResampler(i, o, 2, p).latency()
+        info = g.GetInfo()
+        assert info.Algorithm == b"multi-stage" and info.Latency == g.GetLatency() and info.SIMDEnabled
+
+
+def test_batch_handle_channel_count(gar):
+    g = gar.NewBatch(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True), 1024)
+    assert g.Channels == 2048
+    with pytest.raises(gar.ErrInvalidConfig):
+        gar.NewBatch(gar.Config(44100, 48000, 300, gar.QualityHigh, DryRun=True), 2)

@@ -1,6 +1,6 @@
 """Quick GPU parity sweep used during development (not collected by pytest)."""
 import sys, os, time
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
 sys.path[:0] = [ROOT, os.path.join(ROOT, "go-audio-resampler_amd")]
 import numpy as np, torch
 import gar
