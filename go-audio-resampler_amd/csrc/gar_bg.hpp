@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "gar_kernels.hpp"
+#include "gar_plan.hpp"
 
 namespace gar {
 
@@ -39,16 +40,60 @@ __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, T
 //   macro period a covers outputs [a*Pc, (a+1)*Pc) and reads inputs starting
 //   at a*Qc; a column = (channel c, chunk of G consecutive macro periods);
 //   the workgroup owns 16*ncg columns and stages each column's window of
-//   W = Kc + (G-1)*Qc inputs in LDS (row stride Ws == 2 mod 32 so the 16x4
-//   B-fragment read is bank-conflict free).  Wave (cg, wt) runs tasks
-//   wt, wt+nwt, ... ; a task is one 16-row block (optionally one K slice).
+//   W = Kc + (G-1)*Qc inputs in LDS as [row][16 columns] (the 16x4
+//   B-fragment read is 64 consecutive dwords: bank-conflict free).  The
+//   zero-padded A steps read up to Wl = Kread + (G-1)*Qc >= W rows; rows
+//   [W, Wl) are filled with finite data (A is 0 there, but 0*NaN = NaN).
+//   Wave (cg, wt) runs wave programs wt, wt+nwt, ... (gar_plan.hpp BgProg).
 // ---------------------------------------------------------------------------
 struct BgGrid {
-    int Pc, Qc, Kc, W, Ws, G;
+    int Pc, Qc, Kc, W, Wl, Ws, G;
     int64_t a_lo;
     int nchunk, ncols, nblocks;
-    int C, ntasks, nwt, ncg, ksplit, chan_fast, R;
+    int C, nprog, kch, nwt, ncg, nred, nslots, parity;
+    int dbg;  // development timing knob (GAR_BG_DBG): 1 skip tile DMA after the first, 2 skip stores
+    int vst;  // f32 epilogue: 0 scalar, 1 channel-contiguous (fs == 1), 2 stereo interleaved (C == 2, fs == 2, cs == 1)
 };
+
+// f32 epilogue of one 16x16 accumulator: lane holds rows r0..r0+3 (r0 =
+// rb*16 + 4*(lane>>4)) of column (chunk, c).  vst 1: the four rows are
+// contiguous -> one 16-B store.  vst 2: lanes n, n^1 hold channels 0/1 of the
+// same chunk; they swap halves so each lane stores two whole stereo frames
+// (16 B).  Falls back to checked scalar stores at range edges / misalignment.
+__device__ __forceinline__ void storeRows4(const OutDesc& o, const BgGrid& g, int64_t a, int r0, int c, bool colOk,
+                                           f32x4 v, int lane) {
+    if (g.vst == 2) {
+        const bool even = (lane & 1) == 0;
+        const float s0 = even ? v[2] : v[0], s1 = even ? v[3] : v[1];
+        const float q0 = __shfl_xor(s0, 1), q1 = __shfl_xor(s1, 1);
+        const int rr = even ? r0 : r0 + 2;  // first frame this lane stores
+        f32x4 w;
+        if (even) { w[0] = v[0]; w[1] = q0; w[2] = v[1]; w[3] = q1; }
+        else      { w[0] = q0; w[1] = v[2]; w[2] = q1; w[3] = v[3]; }
+        if (!colOk) return;
+        const int64_t idx = a * g.Pc + rr;
+        float* dst = static_cast<float*>(o.out) + (idx - o.o0) * 2;
+        if (idx >= o.o_lo && idx + 1 < o.o_hi && rr + 1 < g.Pc && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            *reinterpret_cast<f32x4*>(dst) = w;
+        } else {
+            if (rr < g.Pc) { outWrite<float>(o, idx, 0, w[0]); outWrite<float>(o, idx, 1, w[1]); }
+            if (rr + 1 < g.Pc) { outWrite<float>(o, idx + 1, 0, w[2]); outWrite<float>(o, idx + 1, 1, w[3]); }
+        }
+        return;
+    }
+    if (!colOk) return;
+    const int64_t idx = a * g.Pc + r0;
+    if (g.vst == 1) {
+        float* dst = static_cast<float*>(o.out) + (idx - o.o0) + static_cast<int64_t>(c) * o.cs;
+        if (idx >= o.o_lo && idx + 3 < o.o_hi && r0 + 3 < g.Pc && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            *reinterpret_cast<f32x4*>(dst) = v;
+            return;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (r0 + i < g.Pc) outWrite<float>(o, idx + i, c, v[i]);
+}
 
 template <class TC> struct Acc;
 template <> struct Acc<float> {
@@ -116,17 +161,39 @@ __device__ __forceinline__ ColSrc<TC> colSrc(const SrcDesc& s, const BgGrid& g, 
 // writes dword l of the piece, so the LDS image is lane-linear as the DMA
 // requires; each lane fetches from its own column's global address.
 template <class TC>
-__device__ __forceinline__ void loadTile(const SrcDesc& src, const BgGrid& g, int b, TC* sub, int cg, int wt,
-                                         int lane) {
+struct TileSrc {
+    ColSrc<TC> cs;
+    bool allFast;
+};
+
+template <class TC>
+__device__ __forceinline__ TileSrc<TC> tileSrc(const SrcDesc& src, const BgGrid& g, int b, int cg, int lane) {
+    const int n = sizeof(TC) == 8 ? ((lane >> 1) & 15) : (lane & 15);
+    TileSrc<TC> t;
+    t.cs = colSrc<TC>(src, g, b * 16 * g.ncg + cg * 16 + n);
+    t.allFast = __all(t.cs.p != nullptr);
+    return t;
+}
+
+template <class TC>
+__device__ __forceinline__ int tilePieces(const BgGrid& g) {
+    constexpr int rowsPerPiece = sizeof(TC) == 8 ? 2 : 4;
+    return (g.Wl + rowsPerPiece - 1) / rowsPerPiece;
+}
+
+// Issue this wave's DMA pieces j in [jlo, jhi) (j = wt mod nwt) of one sub-tile.
+template <class TC>
+__device__ __forceinline__ void loadPieces(const SrcDesc& src, const BgGrid& g, const TileSrc<TC>& ts, TC* sub,
+                                           int wt, int lane, int jlo, int jhi) {
     constexpr int rowsPerPiece = sizeof(TC) == 8 ? 2 : 4;
     const int n = sizeof(TC) == 8 ? ((lane >> 1) & 15) : (lane & 15);
     const int rsub = sizeof(TC) == 8 ? (lane >> 5) : (lane >> 4);
     const int half = sizeof(TC) == 8 ? (lane & 1) : 0;
-    const ColSrc<TC> cs = colSrc<TC>(src, g, b * 16 * g.ncg + cg * 16 + n);
+    const ColSrc<TC>& cs = ts.cs;
     const bool fast = cs.p != nullptr;
-    const bool allFast = __all(fast);
-    const int npieces = (g.W + rowsPerPiece - 1) / rowsPerPiece;
-    for (int j = wt; j < npieces; j += g.nwt) {
+    const bool allFast = ts.allFast;
+    const int j0 = jlo + ((wt - jlo) % g.nwt + g.nwt) % g.nwt;
+    for (int j = j0; j < jhi; j += g.nwt) {
         int kk = j * rowsPerPiece + rsub;
         TC* dst = sub + static_cast<size_t>(j) * rowsPerPiece * 16;
         if (allFast) {
@@ -144,129 +211,206 @@ __device__ __forceinline__ void loadTile(const SrcDesc& src, const BgGrid& g, in
     }
 }
 
-// prefetch-free kernel: tiles arrive by LDS-DMA while the previous block computes
-template <class TC> struct BgCfg;
-template <> struct BgCfg<float> { static constexpr int kMaxThreads = 640; };
-template <> struct BgCfg<double> { static constexpr int kMaxThreads = 512; };
+template <class TC>
+__device__ __forceinline__ void loadTile(const SrcDesc& src, const BgGrid& g, int b, TC* sub, int cg, int wt,
+                                         int lane) {
+    const TileSrc<TC> ts = tileSrc<TC>(src, g, b, cg, lane);
+    loadPieces<TC>(src, g, ts, sub, wt, lane, 0, tilePieces<TC>(g));
+}
 
+// Generic epilogue of one accumulator (row block rb of macro period a).
+template <class TC>
+__device__ __forceinline__ void storeAcc(const OutDesc& o, const BgGrid& g, int64_t a, int rb, int c, bool colOk,
+                                         const typename Acc<TC>::V& v, int lane) {
+    if constexpr (sizeof(TC) == 4) {
+        storeRows4(o, g, a, rb * 16 + 4 * (lane >> 4), c, colOk, v, lane);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = rb * 16 + Acc<TC>::row(lane, i);
+            if (colOk && r < g.Pc) outWrite<TC>(o, a * g.Pc + r, c, v[i]);
+        }
+    }
+}
+
+// Uniform fields of one wave program (gar_plan.cpp BgPlan::progTable).
+// Scalars only (no runtime-indexed arrays: those would live in scratch).
+struct ProgU {
+    int nseg, e1, e2;
+    int rb0, rb1, rb2, u0, u1, u2, sl0, sl1, sl2, k0, k1, k2;
+};
+
+__device__ __forceinline__ ProgU progLoad(const int* t) {
+    ProgU q;
+    q.nseg = uni(t[0]); q.e1 = uni(t[1]); q.e2 = uni(t[2]);
+    q.rb0 = uni(t[3]); q.u0 = uni(t[4]); q.sl0 = uni(t[5]); q.k0 = uni(t[6]);
+    q.rb1 = uni(t[7]); q.u1 = uni(t[8]); q.sl1 = uni(t[9]); q.k1 = uni(t[10]);
+    q.rb2 = uni(t[11]); q.u2 = uni(t[12]); q.sl2 = uni(t[13]); q.k2 = uni(t[14]);
+    return q;
+}
+
+// Per-step selections (boundaries e1 <= e2 are wave-uniform).
+// Masked arithmetic, not ?: on struct members: clang turns a select of
+// member loads into one load through a selected address (struct in scratch).
+__device__ __forceinline__ int sel3(int s, int e1, int e2, int v0, int v1, int v2) {
+    return v0 + ((v1 - v0) & -static_cast<int>(s >= e1)) + ((v2 - v1) & -static_cast<int>(s >= e2));
+}
+__device__ __forceinline__ int selU(const ProgU& q, int s) { return sel3(s, q.e1, q.e2, q.u0, q.u1, q.u2); }
+__device__ __forceinline__ int selK(const ProgU& q, int s) { return sel3(s, q.e1, q.e2, q.k0, q.k1, q.k2); }
+__device__ __forceinline__ int segRb(const ProgU& q, int j) { return sel3(j, 1, 2, q.rb0, q.rb1, q.rb2); }
+__device__ __forceinline__ int segSlot(const ProgU& q, int j) { return sel3(j, 1, 2, q.sl0, q.sl1, q.sl2); }
+
+// Segment result: direct store (whole row block) or LDS partial slot.
+template <class TC>
+__device__ __forceinline__ void segStore(const ProgU& pu, int j, const typename Acc<TC>::V& r, TC* pslots,
+                                         const OutDesc& od, const BgGrid& g, int64_t a, int c, bool colOk, int lane) {
+    typedef typename Acc<TC>::V V;
+    const int slot = segSlot(pu, j);
+    if (slot < 0) {
+        if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, segRb(pu, j), c, colOk, r, lane);
+    } else {
+        *reinterpret_cast<V*>(pslots + static_cast<size_t>(slot) * 256 + lane * 4) = r;
+    }
+}
+
+// B fragment of program step s: LDS tile, or global memory (GLOBAL_B).
+template <class TC, bool GB>
+__device__ __forceinline__ TC fetchB(const TC* bp, const ProgU& pu, int s, const SrcDesc& src, int64_t tb, int c,
+                                     bool colOk) {
+    if constexpr (GB) return colOk ? srcRead<TC>(src, tb + selK(pu, s) + 4 * s, c) : TC(0);
+    else return bp[selU(pu, s) + 64 * s];
+}
+
+// In-loop segment boundary: bank the running sum (stores happen after the loop).
+// (e1, e2 are segment starts, always inside the program, or 1<<20 if unused)
+#define GAR_SEG_CHECK(s)                                     \
+    if ((s) + 1 == pu.e1) {                                  \
+        r0 = acc0 + acc1; acc0 = V{0, 0, 0, 0}; acc1 = acc0; \
+    } else if ((s) + 1 == pu.e2) {                           \
+        r1 = acc0 + acc1; acc0 = V{0, 0, 0, 0}; acc1 = acc0; \
+    }
+
+// Prefetch-free persistent kernel: the next block's tile arrives by LDS-DMA
+// (issued 1/G per macro-period iteration) while the current block computes.
 template <class TC, int NS, bool GLOBAL_B, bool SINGLE>
-__global__ __launch_bounds__(BgCfg<TC>::kMaxThreads) void bg_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+__global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(BgDev p, SrcDesc src, OutDesc od,
+                                                                               BgGrid g) {
     typedef typename Acc<TC>::V V;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int subElems = g.Ws * 16;                           // one column group's sub-tile
     const int tileElems = GLOBAL_B ? 0 : subElems * g.ncg;
     TC* tiles = reinterpret_cast<TC*>(smem);                 // [2][ncg][Ws][16]
-    TC* part = tiles + 2 * static_cast<size_t>(tileElems);   // k-split partials [ncg][ntasks][256]
+    TC* part = tiles + 2 * static_cast<size_t>(tileElems);   // partials [parity][ncg][nslots][256]
+    const int partStride = g.ncg * g.nslots * 256;
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int cg = wave / g.nwt;
     const int wt = wave - cg * g.nwt;
     const int nloc = cg * 16 + (lane & 15);
+    const int laneOff = (lane >> 4) * 16 + (lane & 15);      // B fragment (k = lane>>4, n = lane&15)
     const TC* Aimg = static_cast<const TC*>(p.A);
 
     TC A[NS];
-    if (SINGLE && wt < g.ntasks) {
+    if (SINGLE && wt < g.nprog) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(wt) * NS + s) * 64 + lane];
     }
 
     int b = blockIdx.x;
     if (!GLOBAL_B && b < g.nblocks) loadTile<TC>(src, g, b, tiles + cg * subElems, cg, wt, lane);
+    int q = 0;  // macro-period iteration counter (partial-slot parity)
     for (int it = 0; b < g.nblocks; b += gridDim.x, ++it) {
         TC* tile = tiles + static_cast<size_t>(it & 1) * tileElems + cg * subElems;
-        __syncthreads();  // waits for this tile's DMA (vmcnt) + frees the other buffer
+        __syncthreads();  // this tile's DMA landed (vmcnt) + the other buffer is free
         const int bn = b + gridDim.x;
-        if (!GLOBAL_B && bn < g.nblocks)
-            loadTile<TC>(src, g, bn, tiles + static_cast<size_t>((it + 1) & 1) * tileElems + cg * subElems, cg, wt, lane);
+        const bool pre = !GLOBAL_B && bn < g.nblocks && !(g.dbg & 1);
+        TC* ntile = tiles + static_cast<size_t>((it + 1) & 1) * tileElems + cg * subElems;
+        TileSrc<TC> nts;
+        if (pre) nts = tileSrc<TC>(src, g, bn, cg, lane);
+        const int np = tilePieces<TC>(g);
 
         const int col = b * 16 * g.ncg + nloc;
         const bool colOk = col < g.ncols;
         const int c = colOk ? col % g.C : 0;
         const int chunk = colOk ? col / g.C : 0;
 
-        for (int gi = 0; gi < g.G; ++gi) {
+        for (int gi = 0; gi < g.G; ++gi, ++q) {
             const int64_t a = g.a_lo + static_cast<int64_t>(chunk) * g.G + gi;
-            for (int t = wt; t < g.ntasks; t += g.nwt) {
-                const int* ti = p.tasks + 5 * t;
-                const int rb = uni(ti[0]), k0 = uni(ti[1]), nks = uni(ti[4]);
-                if (!SINGLE) {
+            // next block's tile: 1/G of its DMA pieces per iteration, so the
+            // LDS-DMA issue interleaves with the MFMA stream instead of bursting
+            if (pre) loadPieces<TC>(src, g, nts, ntile, wt, lane, gi * np / g.G, (gi + 1) * np / g.G);
+            TC* pslots = part + static_cast<size_t>(g.parity ? (q & 1) : 0) * partStride +
+                         static_cast<size_t>(cg) * g.nslots * 256;
+
+            for (int pr = wt; pr < g.nprog; pr += g.nwt) {
+                const ProgU pu = progLoad(p.progs + kBgProgInts * pr);
+                V acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0}, r0 = acc0, r1 = acc0;
+                for (int ch = 0; ch < (SINGLE ? 1 : g.kch); ++ch) {
+                    const int sb = SINGLE ? 0 : ch * NS;  // program step of this chunk's first step
+                    if (!SINGLE) {
 #pragma unroll
-                    for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(t) * NS + s) * 64 + lane];
-                }
-                V acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-                if (GLOBAL_B) {
-                    // window too large for LDS (long decimators): B straight from L1/L2
-                    const int64_t tb = a * g.Qc + k0 + (lane >> 4);
-#pragma unroll
-                    for (int s = 0; s < NS; s += 2) {
-                        acc0 = Acc<TC>::mfma(A[s], colOk ? srcRead<TC>(src, tb + 4 * s, c) : TC(0), acc0);
-                        if (s + 1 < NS)
-                            acc1 = Acc<TC>::mfma(A[s + 1], colOk ? srcRead<TC>(src, tb + 4 * s + 4, c) : TC(0), acc1);
+                        for (int s = 0; s < NS; ++s)
+                            A[s] = Aimg[(static_cast<size_t>(pr) * g.kch * NS + sb + s) * 64 + lane];
                     }
-                } else {
-                    // B fragment (k = lane>>4, n = lane&15) at sub-tile [kk][n]; reads
-                    // software-pipelined 4 steps ahead, sched_barrier keeps the
-                    // compiler from hoisting every ds_read.
-                    const TC* bp = tile + (gi * g.Qc + k0 + (lane >> 4)) * 16 + (lane & 15);
+                    // B reads software-pipelined 4 steps ahead; sched_barrier keeps
+                    // the compiler from hoisting every ds_read.
+                    // (global-B variant: window too large for LDS, B straight from L1/L2)
+                    const TC* bp = tile + gi * g.Qc * 16 + laneOff;
+                    const int64_t tb = a * g.Qc + (lane >> 4);
                     TC bA[4], bB[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) bA[j] = bp[64 * j];
+                    for (int j = 0; j < 4; ++j) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + j, src, tb, c, colOk);
 #pragma unroll
                     for (int s0 = 0; s0 < NS; s0 += 8) {
                         if (s0 + 4 < NS) {
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) bB[j] = bp[64 * (s0 + 4 + j)];
+                            for (int j = 0; j < 4; ++j) bB[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 4 + j, src, tb, c, colOk);
                         }
                         __builtin_amdgcn_sched_barrier(0);
-                        acc0 = Acc<TC>::mfma(A[s0], bA[0], acc0);
-                        acc1 = Acc<TC>::mfma(A[s0 + 1], bA[1], acc1);
-                        acc0 = Acc<TC>::mfma(A[s0 + 2], bA[2], acc0);
-                        acc1 = Acc<TC>::mfma(A[s0 + 3], bA[3], acc1);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int s = s0 + j;
+                            if (j & 1) acc1 = Acc<TC>::mfma(A[s], bA[j], acc1);
+                            else acc0 = Acc<TC>::mfma(A[s], bA[j], acc0);
+                            GAR_SEG_CHECK(sb + s)
+                        }
                         __builtin_amdgcn_sched_barrier(0);
                         if (s0 + 4 < NS) {
                             if (s0 + 8 < NS) {
 #pragma unroll
-                                for (int j = 0; j < 4; ++j) bA[j] = bp[64 * (s0 + 8 + j)];
+                                for (int j = 0; j < 4; ++j) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 8 + j, src, tb, c, colOk);
                             }
                             __builtin_amdgcn_sched_barrier(0);
-                            acc0 = Acc<TC>::mfma(A[s0 + 4], bB[0], acc0);
-                            acc1 = Acc<TC>::mfma(A[s0 + 5], bB[1], acc1);
-                            acc0 = Acc<TC>::mfma(A[s0 + 6], bB[2], acc0);
-                            acc1 = Acc<TC>::mfma(A[s0 + 7], bB[3], acc1);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const int s = s0 + 4 + j;
+                                if (j & 1) acc1 = Acc<TC>::mfma(A[s], bB[j], acc1);
+                                else acc0 = Acc<TC>::mfma(A[s], bB[j], acc0);
+                                GAR_SEG_CHECK(sb + s)
+                            }
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
                 }
-                const V acc = acc0 + acc1;
-                if (nks == 1) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = rb * 16 + Acc<TC>::row(lane, i);
-                        if (colOk && r < g.Pc) outWrite<TC>(od, a * g.Pc + r, c, acc[i]);
-                    }
-                } else {
-                    TC* slot = part + (static_cast<size_t>(cg) * g.ntasks + t) * 256 + lane * 4;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) slot[i] = acc[i];
-                }
+                const V rl = acc0 + acc1;
+                segStore<TC>(pu, 0, pu.nseg > 1 ? r0 : rl, pslots, od, g, a, c, colOk, lane);
+                if (pu.nseg > 1) segStore<TC>(pu, 1, pu.nseg > 2 ? r1 : rl, pslots, od, g, a, c, colOk, lane);
+                if (pu.nseg > 2) segStore<TC>(pu, 2, rl, pslots, od, g, a, c, colOk, lane);
             }
-            if (g.ksplit) {
-                __syncthreads();
-                for (int t = wt; t < g.ntasks; t += g.nwt) {
-                    const int* ti = p.tasks + 5 * t;
-                    if (uni(ti[4]) == 1 || uni(ti[3]) != 0) continue;
-                    const int rb = uni(ti[0]), nks = uni(ti[4]);
-                    const TC* slot = part + (static_cast<size_t>(cg) * g.ntasks + t) * 256 + lane * 4;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        TC sum = slot[i];
-                        for (int k = 1; k < nks; ++k) sum += slot[k * 256 + i];
-                        const int r = rb * 16 + Acc<TC>::row(lane, i);
-                        if (colOk && r < g.Pc) outWrite<TC>(od, a * g.Pc + r, c, sum);
-                    }
+            if (g.nred > 0) {
+                __syncthreads();  // partial slots of this macro period written
+                for (int r = wt; r < g.nred; r += g.nwt) {
+                    const int* rt = p.reds + kBgRedInts * r;
+                    const int rb = uni(rt[0]), n = uni(rt[1]);
+                    V sum = *reinterpret_cast<const V*>(pslots + static_cast<size_t>(uni(rt[2])) * 256 + lane * 4);
+                    for (int k = 1; k < n; ++k)
+                        sum += *reinterpret_cast<const V*>(pslots + static_cast<size_t>(uni(rt[2 + k])) * 256 + lane * 4);
+                    if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
                 }
-                __syncthreads();
+                // with two slot buffers the next iteration writes the other one;
+                // its barrier orders this reduction before the buffer's reuse
+                if (!g.parity) __syncthreads();
             }
         }
     }
@@ -281,10 +425,15 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, false>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, true>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, false>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attrSet = true;
     }
+    if (threads > bgMaxThreads(sizeof(TC) == 8, NS)) return hipErrorInvalidConfiguration;
     const dim3 gd(static_cast<unsigned>(blocks)), bd(threads);
-    const bool single = g.ntasks <= g.nwt;
+    const bool single = g.kch == 1;
     if (globalB) {
         if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, true, true>), gd, bd, lds, st, p, src, od, g);
         else hipLaunchKernelGGL((bg_kernel<TC, NS, true, false>), gd, bd, lds, st, p, src, od, g);

@@ -89,16 +89,23 @@ struct StageRT {
 BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
     BgDev d{};
     d.f64 = p.f64 ? 1 : 0;
-    d.Pc = p.Pc; d.Qc = p.Qc; d.Kc = p.Kc; d.NS = p.NS; d.nrb = p.nrb;
-    d.ntasks = static_cast<int>(p.tasks.size());
-    d.ksplit = p.ksplit ? 1 : 0;
+    d.Pc = p.Pc; d.Qc = p.Qc; d.Kc = p.Kc; d.Kread = p.Kread; d.NS = p.NS; d.nrb = p.nrb;
+    d.nprog = static_cast<int>(p.progs.size());
+    d.kch = p.kch;
+    d.nw = p.nw;
+    d.ncg = p.ncg;
+    d.nred = static_cast<int>(p.reds.size());
+    d.nslots = p.nslots;
     if (dry) return d;
     if (p.f64) A.upload(p.A64); else A.upload(p.A32);
-    std::vector<int> t;
-    for (const auto& k : p.tasks) { t.push_back(k.rb); t.push_back(k.k0); t.push_back(k.ns); t.push_back(k.ks); t.push_back(k.nks); }
+    std::vector<int> t = p.progTable();
+    const std::vector<int> rt = p.redTable();
+    const size_t redOff = t.size();
+    t.insert(t.end(), rt.begin(), rt.end());
     T.upload(t);
     d.A = A.p;
-    d.tasks = static_cast<const int*>(T.p);
+    d.progs = static_cast<const int*>(T.p);
+    d.reds = static_cast<const int*>(T.p) + redOff;
     return d;
 }
 
@@ -277,8 +284,8 @@ struct gar_resampler {
     bool profile = false;
     struct Ev { int tag; hipEvent_t a, b; };
     std::vector<Ev> events;
-    double profiledMs[3] = {0, 0, 0};
-    int64_t profiledLaunches[3] = {0, 0, 0};
+    double profiledMs[4] = {0, 0, 0, 0};
+    int64_t profiledLaunches[4] = {0, 0, 0, 0};
 };
 
 namespace gar {
@@ -489,7 +496,7 @@ int64_t stageFlush(Ctx& x, int si, const OutView& out) {
                 if (t.poly_hist > 0) nB = cntPoly(t, d.poly, d.poly.taps, quirk);
                 if (!quirk) {
                     const int64_t y0 = c.y_count, n = nA + nB;
-                    if (x.launch && n > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, n), C));
+                    if (x.launch && n > 0) HIPCHK(timedBg(x, 3, rt.fusedD, xsrc, mkOut(out, y0, n), C));
                     c = t;
                     c.y_count = y0 + n;
                     c.staged = true;
@@ -1189,7 +1196,7 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
 }
 
 gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t* launches) {
-    if (!r || kind < 0 || kind > 2) return GAR_ERR_INVALID_ARGUMENT;
+    if (!r || kind < 0 || kind > 3) return GAR_ERR_INVALID_ARGUMENT;
     return wrap([&]() -> gar_status {
         for (auto& ev : r->events) {
             HIPCHK(hipEventSynchronize(ev.b));

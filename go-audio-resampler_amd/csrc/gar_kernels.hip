@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "gar_bg.hpp"
 #include "gar_kernels.hpp"
@@ -30,46 +31,63 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;
-    g.ntasks = p.ntasks;
-    const int maxw = p.f64 ? 8 : 10;
-    g.nwt = p.ntasks < maxw ? p.ntasks : maxw;
-    g.ncg = 1;
-    while (g.ncg * 2 * g.nwt <= 8 && g.ncg < 4) g.ncg *= 2;  // fill >= 4 waves per workgroup
-    g.ksplit = p.ksplit;
+    // Tuning knobs (development sweeps only; defaults are the tuned values).
+    static const int knobG = std::getenv("GAR_BG_G") ? std::atoi(std::getenv("GAR_BG_G")) : 0;
+    static const int knobWgPerCu = std::getenv("GAR_BG_WGPERCU") ? std::atoi(std::getenv("GAR_BG_WGPERCU")) : 0;
+    static const int knobDbg = std::getenv("GAR_BG_DBG") ? std::atoi(std::getenv("GAR_BG_DBG")) : 0;
+    static const bool knobNoVst = std::getenv("GAR_BG_NOVST") != nullptr;
+    static const bool knobNoParity = std::getenv("GAR_BG_NOPARITY") != nullptr;
+    g.nprog = p.nprog;
+    g.kch = p.kch;
+    g.nwt = p.nw;
+    g.ncg = p.ncg;
+    g.nred = p.nred;
+    g.nslots = p.nslots;
     g.a_lo = od.o_lo / p.Pc;
     const int64_t a_hi = (od.o_hi + p.Pc - 1) / p.Pc;
     const int64_t nmac = a_hi - g.a_lo;
     const int threads = 64 * g.ncg * g.nwt;
     const int tileN = 16 * g.ncg;
-    const size_t partBytes = g.ksplit ? static_cast<size_t>(g.ncg) * g.ntasks * 256 * sz : 0;
-    // Two LDS tiles (double buffer) within 160 KiB.
+    const size_t slotBytes = static_cast<size_t>(g.ncg) * g.nslots * 256 * sz;
+    // Two LDS tiles (double buffer) + partial slots (two buffers when they fit
+    // beside a tile of >= 4 macro periods, else one + a second barrier).
     const int rowsPerPiece = p.f64 ? 2 : 4;
     auto wsFor = [&](int W) { return (W + rowsPerPiece - 1) / rowsPerPiece * rowsPerPiece; };
+    auto tileBytes = [&](int G) { return 2 * static_cast<size_t>(tileN) * wsFor(p.Kread + (G - 1) * p.Qc) * sz; };
+    const size_t kLds = 160 * 1024;
+    g.parity = (g.nred > 0 && !knobNoParity && tileBytes(std::min<int64_t>(4, std::max<int64_t>(nmac, 1))) + 2 * slotBytes <= kLds) ? 1 : 0;
+    const size_t partBytes = (g.parity ? 2 : 1) * slotBytes;
     int G = 1;
     for (int cand = 2; cand <= 8; ++cand) {
         if (cand > nmac) break;
-        const int W = p.Kc + (cand - 1) * p.Qc;
-        if (2 * static_cast<size_t>(tileN) * wsFor(W) * sz + partBytes > 160 * 1024) break;
+        if (tileBytes(cand) + partBytes > kLds) break;
         G = cand;
     }
+    if (knobG > 0 && knobG < G) G = knobG;
     g.G = G;
     g.W = p.Kc + (G - 1) * p.Qc;
-    g.Ws = wsFor(g.W);
+    g.Wl = p.Kread + (G - 1) * p.Qc;
+    g.Ws = wsFor(g.Wl);
     const int64_t nchunk = (nmac + G - 1) / G;
     g.nchunk = static_cast<int>(nchunk);
     g.ncols = static_cast<int>(nchunk * C);
     g.nblocks = (g.ncols + tileN - 1) / tileN;
-    g.chan_fast = C >= 16 ? 1 : 0;
-    g.R = 0;
-    size_t lds = 2 * static_cast<size_t>(tileN) * g.Ws * sz + partBytes;
-    const bool globalB = lds > 160 * 1024;
+    g.dbg = knobDbg;
+    g.vst = 0;
+    if (!p.f64 && !od.f64 && !knobNoVst) {
+        if (od.fs == 1) g.vst = 1;
+        else if (C == 2 && od.fs == 2 && od.cs == 1) g.vst = 2;
+    }
+    size_t lds = tileBytes(G) + partBytes;
+    const bool globalB = lds > kLds;
     if (globalB) lds = partBytes;
+    if (lds > kLds) return hipErrorInvalidConfiguration;
     if (g.nblocks <= 0) return hipSuccess;
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    int64_t blocks = std::min<int64_t>(g.nblocks, static_cast<int64_t>(ncu) * 2);
+    int64_t blocks = std::min<int64_t>(g.nblocks, static_cast<int64_t>(ncu) * (knobWgPerCu > 0 ? knobWgPerCu : 2));
     if (p.f64) return bgLaunchF64(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
-    if (p.NS < 60) return bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
+    if (p.NS < 56) return bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
     return bgLaunchF32b(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
 }
 

@@ -32,9 +32,11 @@ struct OutDesc {
 // Device copy of a BgPlan (gar_plan.hpp).
 struct BgDev {
     int f64;
-    int Pc, Qc, Kc, NS, nrb, ntasks, ksplit;
-    const void* A;      // [ntasks][NS][64]
-    const int* tasks;   // [ntasks][5] = rb, k0, ns, ks, nks
+    int Pc, Qc, Kc, Kread, NS, nrb;
+    int nprog, kch, nw, ncg, nred, nslots;
+    const void* A;      // [nprog][kch*NS][64]
+    const int* progs;   // [nprog][kBgProgInts] (gar_plan.hpp BgPlan::progTable)
+    const int* reds;    // [nred][kBgRedInts]
 };
 
 // General polyphase stage with live cubic coefficient interpolation

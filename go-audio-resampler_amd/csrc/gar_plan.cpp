@@ -112,6 +112,87 @@ std::vector<RbGeom> geomFor(const FirPeriodic& f, int mp, double& eff) {
 }
 }  // namespace
 
+namespace {
+// Even split of the row blocks' steps over nprog programs (<= kBgMaxSeg
+// segments each); row blocks cut across programs get LDS slots + a reduction.
+bool splitPrograms(const std::vector<RbGeom>& rbs, int nprog, std::vector<BgProg>& progs, std::vector<BgRed>& reds,
+                   int& nslots, int& maxLen) {
+    int64_t S = 0;
+    for (const auto& r : rbs) S += r.nsteps;
+    const int T = static_cast<int>((S + nprog - 1) / nprog);
+    progs.assign(nprog, BgProg());
+    reds.clear();
+    int w = 0;
+    std::vector<std::vector<std::pair<int, int>>> owners(rbs.size());  // rb -> (prog, seg)
+    for (size_t rb = 0; rb < rbs.size(); ++rb) {
+        int pos = 0, rem = rbs[rb].nsteps;
+        while (rem > 0) {
+            if (w >= nprog) return false;
+            BgProg& pg = progs[w];
+            if (pg.nseg == kBgMaxSeg) return false;
+            const int take = std::min(rem, T - pg.len);
+            BgSeg& sg = pg.seg[pg.nseg];
+            sg.rb = static_cast<int>(rb);
+            sg.k0 = rbs[rb].klo + 4 * pos;
+            sg.ns = take;
+            sg.start = pg.len;
+            owners[rb].push_back({w, pg.nseg});
+            pg.nseg++;
+            pg.len += take;
+            pos += take;
+            rem -= take;
+            if (pg.len == T) ++w;
+        }
+    }
+    nslots = 0;
+    for (size_t rb = 0; rb < rbs.size(); ++rb) {
+        if (owners[rb].size() <= 1) continue;
+        if (owners[rb].size() > static_cast<size_t>(kBgMaxRedSlots)) return false;
+        BgRed r;
+        r.rb = static_cast<int>(rb);
+        for (const auto& o : owners[rb]) {
+            progs[o.first].seg[o.second].slot = nslots;
+            r.slot[r.n++] = nslots++;
+        }
+        reds.push_back(r);
+    }
+    maxLen = 0;
+    for (const auto& pg : progs) maxLen = std::max(maxLen, pg.len);
+    return true;
+}
+}  // namespace
+
+std::vector<int> BgPlan::progTable() const {
+    std::vector<int> t(progs.size() * kBgProgInts, 0);
+    for (size_t i = 0; i < progs.size(); ++i) {
+        int* e = &t[i * kBgProgInts];
+        const BgProg& pg = progs[i];
+        e[0] = pg.nseg;
+        // in-loop flush boundaries (the last segment runs to NS and flushes after the loop)
+        e[1] = pg.nseg >= 2 ? pg.seg[1].start : 1 << 20;
+        e[2] = pg.nseg >= 3 ? pg.seg[2].start : 1 << 20;
+        for (int j = 0; j < kBgMaxSeg; ++j) {
+            const BgSeg& sg = pg.seg[j];
+            e[3 + 4 * j] = sg.rb;
+            e[4 + 4 * j] = (sg.k0 - 4 * sg.start) * 16;   // LDS element offset so step s reads +64*s
+            e[5 + 4 * j] = sg.slot;
+            e[6 + 4 * j] = sg.k0 - 4 * sg.start;          // input offset (global-B path)
+        }
+    }
+    return t;
+}
+
+std::vector<int> BgPlan::redTable() const {
+    std::vector<int> t(reds.size() * kBgRedInts, 0);
+    for (size_t i = 0; i < reds.size(); ++i) {
+        int* e = &t[i * kBgRedInts];
+        e[0] = reds[i].rb;
+        e[1] = reds[i].n;
+        for (int k = 0; k < reds[i].n; ++k) e[2 + k] = reds[i].slot[k];
+    }
+    return t;
+}
+
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     if (f.P <= 0 || f.Q <= 0) return false;
     // Pick the macro period (multiple of the FIR period) with the best
@@ -134,48 +215,65 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     plan.Pc = f.P * bestMp;
     plan.Qc = f.Q * bestMp;
     plan.nrb = static_cast<int>(rbs.size());
-    const int maxNS = f64 ? 48 : 112;
-    int needNS = 0;
-    for (int rb = 0; rb < plan.nrb; ++rb) {
-        const int nst = rbs[rb].nsteps;
-        const int nks = (nst + maxNS - 1) / maxNS;
-        const int per = (nst + nks - 1) / nks;
-        for (int ks = 0; ks < nks; ++ks) {
-            BgTask t;
-            t.rb = rb;
-            t.ks = ks;
-            t.nks = nks;
-            t.k0 = rbs[rb].klo + 4 * ks * per;
-            t.ns = std::min(per, nst - ks * per);
-            plan.tasks.push_back(t);
-            needNS = std::max(needNS, t.ns);
-        }
-        if (nks > 1) plan.ksplit = true;
-        plan.Kc = std::max(plan.Kc, rbs[rb].klo + 4 * nst);
-    }
-    // Kernel instantiations exist for NS = 8, 12, ..., maxNS; the A image is
-    // zero padded to NS steps so the MFMA loop has no per-step guard.
-    plan.NS = std::max(8, (needNS + 3) / 4 * 4);
-    if (plan.NS > maxNS) return false;
+    for (const auto& r : rbs) plan.Kc = std::max(plan.Kc, r.klo + 4 * r.nsteps);
 
-    const size_t nt = plan.tasks.size();
-    const size_t img = nt * plan.NS * 64;
-    std::vector<double> A(img, 0.0);
-    for (size_t ti = 0; ti < nt; ++ti) {
-        const BgTask& t = plan.tasks[ti];
-        for (int s = 0; s < t.ns; ++s)
-            for (int lane = 0; lane < 64; ++lane) {
-                const int m = lane & 15, kq = lane >> 4;
-                const int r = t.rb * 16 + m;
-                if (r >= plan.Pc) continue;
-                int64_t off;
-                const std::vector<double>* row;
-                macroRow(f, r, off, row);
-                const int64_t kk = t.k0 + 4 * s + kq;
-                const int64_t idx = kk - off;
-                if (idx >= 0 && idx < static_cast<int64_t>(row->size()))
-                    A[(ti * plan.NS + s) * 64 + lane] = (*row)[idx];
+    // Choose waves per column group (nw) and column groups (ncg) minimising
+    // the critical SIMD's MFMA steps per column:
+    //   ceil(waves/4) * kch*NS / (16 * ncg), x latency factor for < 3 waves/SIMD
+    // (a program longer than maxNS runs as kch chunks of NS steps).
+    const int maxNS = f64 ? 48 : 96;
+    double bestCost = 1e300;
+    for (int nw = 1; nw <= 16; ++nw) {
+        std::vector<BgProg> progs;
+        std::vector<BgRed> reds;
+        int nslots = 0, maxLen = 0;
+        if (!splitPrograms(rbs, nw, progs, reds, nslots, maxLen)) continue;
+        const int kch = (maxLen + maxNS - 1) / maxNS;
+        const int NS = std::max(8, ((maxLen + kch - 1) / kch + 3) / 4 * 4);
+        for (int ncg = 1; ncg <= 4; ncg *= 2) {
+            const int waves = nw * ncg;
+            if (waves > 16 || 64 * waves > bgMaxThreads(f64, NS)) continue;
+            const int wps = (waves + 3) / 4;
+            const double lat = wps == 1 ? 1.4 : (wps == 2 ? 1.1 : 1.0);
+            const double cost = static_cast<double>(wps) * NS * kch / (16.0 * ncg) * lat * (kch > 1 ? 1.2 : 1.0) *
+                                (1.0 + 0.01 * static_cast<double>(reds.size()));
+            if (cost < bestCost - 1e-9) {
+                bestCost = cost;
+                plan.nw = nw;
+                plan.ncg = ncg;
+                plan.NS = NS;
+                plan.kch = kch;
+                plan.progs = progs;
+                plan.reds = reds;
+                plan.nslots = nslots;
             }
+        }
+    }
+    if (plan.progs.empty()) return false;
+
+    const size_t np = plan.progs.size();
+    const int plen = plan.kch * plan.NS;  // steps per program incl. padding
+    std::vector<double> A(np * plen * 64, 0.0);
+    plan.Kread = plan.Kc;
+    for (size_t pi = 0; pi < np; ++pi) {
+        const BgProg& pg = plan.progs[pi];
+        for (int j = 0; j < pg.nseg; ++j) {
+            const BgSeg& sg = pg.seg[j];
+            const int runLen = j == pg.nseg - 1 ? plen - sg.start : sg.ns;  // last segment runs to the end
+            plan.Kread = std::max(plan.Kread, sg.k0 + 4 * runLen);
+            for (int s = 0; s < sg.ns; ++s)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int m = lane & 15, kq = lane >> 4;
+                    const int r = sg.rb * 16 + m;
+                    if (r >= plan.Pc) continue;
+                    int64_t off;
+                    const std::vector<double>* row;
+                    macroRow(f, r, off, row);
+                    const int64_t idx = sg.k0 + 4 * s + kq - off;
+                    if (idx >= 0 && idx < static_cast<int64_t>(row->size()))
+                        A[(pi * plen + sg.start + s) * 64 + lane] = (*row)[idx];
+                }
+        }
     }
     if (f64) plan.A64 = std::move(A);
     else plan.A32.assign(A.begin(), A.end());
@@ -184,7 +282,7 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     for (const auto& r : f.rows) useful += static_cast<double>(r.size());
     plan.usefulMacsPerOutput = useful / f.P;
     double exec = 0;
-    for (const auto& t : plan.tasks) exec += 16.0 * 4.0 * t.ns;  // per column per macro period
+    for (const auto& r : rbs) exec += 16.0 * 4.0 * r.nsteps;  // per column per macro period
     plan.mfmaMacsPerOutput = exec / plan.Pc;
     return true;
 }

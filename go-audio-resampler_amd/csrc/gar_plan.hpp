@@ -30,8 +30,28 @@ FirPeriodic firFromDecim(const DecimBank& d);
 bool firFromPoly(const PolyBank& p, FirPeriodic& out);                          // needs fracFree()
 bool firComposite(const DftBank& d, const PolyBank& p, FirPeriodic& out);       // needs factor 2 + fracFree()
 
-// Task = (row block, K slice) executed by one wavefront.
-struct BgTask { int rb, k0, ns, ks, nks; };
+// Wave program = the MFMA steps one wavefront runs per macro period: up to 3
+// segments, each a contiguous K range of one row block.  The total step count
+// of all row blocks is split evenly over the programs so every SIMD carries
+// the same MFMA load; a row block cut across programs is finished by an LDS
+// reduction of its partial accumulators (slot >= 0).  A program longer than
+// the register budget runs as kch chunks of NS steps (A re-read per chunk).
+constexpr int kBgMaxSeg = 3;
+constexpr int kBgMaxRedSlots = 16;
+constexpr int kBgProgInts = 16;                    // device table stride
+constexpr int kBgRedInts = 2 + kBgMaxRedSlots;
+
+struct BgSeg { int rb = 0, k0 = 0, ns = 0, start = 0, slot = -1; };
+struct BgProg { int nseg = 0, len = 0; BgSeg seg[kBgMaxSeg]; };
+struct BgRed { int rb = 0, n = 0; int slot[kBgMaxRedSlots] = {}; };
+
+// Register budget of the kernel instantiation for NS steps -> the largest
+// workgroup it may be launched with (__launch_bounds__).  Overheads measured
+// with -Rpass-analysis=kernel-resource-usage (no spills at these bounds).
+constexpr int bgMaxThreads(bool f64, int NS) {
+    return f64 ? (2 * NS + 140 <= 128 ? 1024 : (2 * NS + 140 <= 168 ? 768 : 512))
+               : (NS + 92 <= 128 ? 1024 : (NS + 92 <= 168 ? 768 : 512));
+}
 
 struct BgPlan {
     bool f64 = false;
@@ -39,16 +59,23 @@ struct BgPlan {
     int Pc = 0, Qc = 0;               // outputs / inputs per macro period
     int nrb = 0;                      // row blocks of 16 outputs
     int Kc = 0;                       // input window (elements) one macro period needs
-    int NS = 0;                       // steps per task (template bucket)
-    bool ksplit = false;
-    std::vector<BgTask> tasks;
-    std::vector<float> A32;           // [ntasks][NS][64] MFMA A fragments
+    int Kread = 0;                    // rows the zero-padded MFMA loop reads (>= Kc)
+    int NS = 0;                       // steps per chunk (template bucket); a program is kch chunks
+    int kch = 1;                      // chunks per program (> 1: A re-read per chunk, long filters)
+    int nw = 1;                       // waves (= programs) per column group
+    int ncg = 1;                      // column groups (16 columns each) per workgroup
+    int nslots = 0;                   // LDS partial slots per column group
+    std::vector<BgProg> progs;        // [nw]
+    std::vector<BgRed> reds;          // row blocks finished by reduction
+    std::vector<float> A32;           // [nw][kch*NS][64] MFMA A fragments
     std::vector<double> A64;
     double usefulMacsPerOutput = 0;   // sum of row lengths / P
-    double mfmaMacsPerOutput = 0;     // executed MFMA MACs / output (incl. band padding)
+    double mfmaMacsPerOutput = 0;     // MFMA MACs / output over the band (excl. bucket padding)
+    std::vector<int> progTable() const;  // [nprog][kBgProgInts]
+    std::vector<int> redTable() const;   // [nred][kBgRedInts]
 };
 
-// Builds the MFMA plan; maxNS bounds steps per task (register budget).
+// Builds the MFMA plan (macro period, balanced wave programs, A image).
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
 
 }  // namespace gar

@@ -167,7 +167,8 @@ const char *gar_last_error(void);                       /* thread-local detail f
 /* HIP-event timing of every MFMA FIR launch (bracketed on its own stream). */
 void gar_profile_enable(gar_resampler *r, int32_t on);
 /* Sum of launch durations (ms) and launch count of one kernel kind (0 fused
- * DFT+polyphase FIR, 1 DFT FIR, 2 decimator FIR) since its last read. */
+ * DFT+polyphase FIR, 1 DFT FIR, 2 decimator FIR, 3 fused FIR launched by a
+ * flush) since its last read. */
 gar_status gar_profile_read(gar_resampler *r, int32_t kind, double *ms, int64_t *launches);
 
 /* ---- host-only design introspection (no GPU needed) ----------------------- */
