@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -82,9 +83,54 @@ struct StageRT {
     BgDev fusedD{}, dftD{}, decimD{};
     DevBuf pa, pb, pc, pd;
     PolyDev polyD{};
+    // split-f16 variants (f32 compute), referenced from the BgDev's .hx
+    struct HxRT {
+        HxPlan plan;
+        DevBuf A, T, rows, roff, rlen, fix;
+        HxDev d{};
+    } fusedH, dftH, decimH;
 
     int tc() const { return f64 ? 8 : 4; }
 };
+
+// Builds + uploads the split-f16 plan of `f` and points bg.hx at it.
+bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry) {
+    if (!buildHxPlan(f, h.plan)) return false;
+    HxDev& d = h.d;
+    const HxPlan& p = h.plan;
+    // two double-buffered hi/lo images of one macro period + one partial-slot buffer must fit LDS;
+    // longer filters (e.g. the 1223-tap decimator) stay on the exact-f32 kernel
+    const size_t ws1 = (static_cast<size_t>(p.Kread) + 7) / 8 * 8;
+    if (ws1 > static_cast<size_t>(kHxMaxRows)) return false;
+    if (4 * ws1 * 32 + static_cast<size_t>(p.nslots) * 256 * 4 + 128 > 160 * 1024) return false;
+    d = HxDev{};
+    d.Pc = p.Pc; d.Qc = p.Qc; d.Kc = p.Kc; d.Kread = p.Kread; d.NS = p.NS; d.nrb = p.nrb;
+    d.nw = p.nw; d.kch = p.kch; d.nred = static_cast<int>(p.reds.size()); d.nslots = p.nslots;
+    d.ea = p.ea; d.rowMax = p.rowMax; d.rb = p.rbMode ? 1 : 0;
+    if (!dry) {
+        h.A.upload(p.A);
+        std::vector<int> t = p.progTable();
+        const std::vector<int> rt = p.redTable();
+        const size_t redOff = t.size();
+        t.insert(t.end(), rt.begin(), rt.end());
+        h.T.upload(t);
+        h.rows.upload(p.rows);
+        h.roff.upload(p.rowOff);
+        h.rlen.upload(p.rowLen);
+        d.A = h.A.p;
+        d.progs = static_cast<const int*>(h.T.p);
+        d.reds = static_cast<const int*>(h.T.p) + redOff;
+        d.rows = static_cast<const float*>(h.rows.p);
+        d.rowOff = static_cast<const int*>(h.roff.p);
+        d.rowLen = static_cast<const int*>(h.rlen.p);
+        d.fixCap = 4096;
+        h.fix.upload(std::vector<int>(2 + d.fixCap + 64, 0));
+        d.fix = static_cast<int*>(h.fix.p);
+        d.zero = reinterpret_cast<const float*>(d.fix + 2 + d.fixCap);  // 64 zero words past the list
+    }
+    bg.hx = &h.d;
+    return true;
+}
 
 BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
     BgDev d{};
@@ -115,22 +161,26 @@ void uploadBank(const std::vector<double>& v, DevBuf& b) {
     b.upload(c);
 }
 
-bool buildStage(StageRT& s, bool f64, bool dry, std::string& err) {
+bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
     s.f64 = f64;
+    hx = hx && !f64;
     const EngineDesign& d = s.d;
     if (d.kind == EngineKind::Cubic) { err = "QualityQuick cubic stage is not supported on the GPU path yet"; return false; }
     if (d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) {
         if (!buildBgPlan(firFromDft(d.dft), f64, s.dftP)) { err = "DFT plan"; return false; }
         s.dftD = uploadPlan(s.dftP, s.dftA, s.dftT, dry);
+        if (hx) attachHx(firFromDft(d.dft), s.dftH, s.dftD, dry);
     }
     if (d.kind == EngineKind::Decim) {
         if (!buildBgPlan(firFromDecim(d.decim), f64, s.decimP)) { err = "decimator plan"; return false; }
         s.decimD = uploadPlan(s.decimP, s.decimA, s.decimT, dry);
+        if (hx) attachHx(firFromDecim(d.decim), s.decimH, s.decimD, dry);
     }
     if (d.kind == EngineKind::DftPoly) {
         if (firComposite(d.dft, d.poly, s.compositeFir) && buildBgPlan(s.compositeFir, f64, s.fusedP)) {
             s.fused = true;
             s.fusedD = uploadPlan(s.fusedP, s.fusedA, s.fusedT, dry);
+            if (hx) attachHx(s.compositeFir, s.fusedH, s.fusedD, dry);
         }
         PolyDev& p = s.polyD;
         p.f64 = f64 ? 1 : 0;
@@ -271,6 +321,7 @@ struct gar_resampler {
     int channels = 1;      // total (streams * channels for a batch)
     double ratio = 1.0;
     bool f64 = true;       // compute dtype
+    bool hx = false;       // f32 compute on the split-f16 MFMA kernel (GAR_F32) instead of exact-f32 MFMA
     bool dry = false;
     int device = 0;
     bool engineF32Io = false;
@@ -758,6 +809,15 @@ gar_status validate(const gar_config* c) {
     return GAR_OK;
 }
 
+// GAR_HX=0 in the environment routes GAR_F32 compute to the exact-f32 MFMA kernel (A/B comparisons).
+bool hxEnabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("GAR_HX");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 gar_status initDevice(Handle* h) {
     if (h->dry) return GAR_OK;
     int n = 0;
@@ -774,7 +834,7 @@ gar_status addStage(Handle* h, double inRate, double outRate, Quality q) {
     auto rt = std::make_unique<StageRT>();
     std::string err;
     if (!designEngine(inRate, outRate, q, rt->d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
-    if (!buildStage(*rt, h->f64, h->dry, err)) {
+    if (!buildStage(*rt, h->f64, h->hx, h->dry, err)) {
         g_err = err;
         return rt->d.kind == EngineKind::Cubic ? GAR_ERR_NOT_SUPPORTED : GAR_ERR_INTERNAL;
     }
@@ -794,7 +854,8 @@ gar_status newCommon(gar_config* cfg, int32_t nstreams, gar_resampler** out) {
     h->cfg = *cfg;
     h->channels = cfg->channels * nstreams;
     h->ratio = cfg->output_rate / cfg->input_rate;
-    h->f64 = cfg->compute_dtype != GAR_F32;
+    h->f64 = cfg->compute_dtype != GAR_F32 && cfg->compute_dtype != GAR_F32_EXACT;
+    h->hx = cfg->compute_dtype == GAR_F32 && hxEnabled();
     h->dry = cfg->dry_run != 0;
     h->device = cfg->device;
     return wrap([&]() -> gar_status {
@@ -901,6 +962,7 @@ gar_status gar_new_engine(double in_rate, double out_rate, int32_t preset, int32
     h->newPath = false;
     h->channels = 1;
     h->f64 = dtype != GAR_F32;
+    h->hx = dtype == GAR_F32 && hxEnabled();
     h->engineF32Io = dtype == GAR_F32;
     if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
     h->ratio = out_rate / in_rate;
@@ -924,6 +986,7 @@ gar_status gar_new_engine_dry(double in_rate, double out_rate, int32_t preset, i
     h->newPath = false;
     h->dry = true;
     h->f64 = dtype != GAR_F32;
+    h->hx = dtype == GAR_F32 && hxEnabled();
     if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
     return wrap([&]() -> gar_status {
         gar_status st = addStage(h.get(), in_rate, out_rate, presetToEngineQuality(preset));

@@ -28,6 +28,8 @@ hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
+    // f32 compute on the split-f16 kernel; f64 input (float64 API on a float32 engine) stays on exact f32
+    if (p.hx && !p.f64 && !src.in_f64) return launchHx(*p.hx, src, od, C, stream);
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;

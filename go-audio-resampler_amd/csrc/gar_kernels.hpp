@@ -29,6 +29,8 @@ struct OutDesc {
     int64_t o_lo, o_hi;
 };
 
+struct HxDev;
+
 // Device copy of a BgPlan (gar_plan.hpp).
 struct BgDev {
     int f64;
@@ -37,6 +39,23 @@ struct BgDev {
     const void* A;      // [nprog][kch*NS][64]
     const int* progs;   // [nprog][kBgProgInts] (gar_plan.hpp BgPlan::progTable)
     const int* reds;    // [nred][kBgRedInts]
+    const HxDev* hx;    // host pointer: split-f16 variant of this plan (f32 compute) or null
+};
+
+// Device copy of an HxPlan (gar_plan.hpp): split-f16 MFMA FIR, f32 compute.
+struct HxDev {
+    int Pc, Qc, Kc, Kread, NS, nrb;
+    int nw, kch, nred, nslots, ea, rowMax;
+    int rb;              // row-block mode (HxPlan::rbMode)
+    int fixCap;          // capacity of the non-finite block list
+    int* fix;            // [2 + fixCap]: count, finished workgroups, block ids (zero between launches)
+    const float* zero;   // a zero float (LDS-DMA source of flush zeros / out-of-range rows)
+    const void* A;       // [nw][kch*NS][2][64][8] f16
+    const int* progs;    // [nw][kBgProgInts] (HxPlan::progTable)
+    const int* reds;     // [nred][kBgRedInts]
+    const float* rows;   // non-finite fallback rows [Pc][rowMax]
+    const int* rowOff;   // [Pc]
+    const int* rowLen;   // [Pc]
 };
 
 // General polyphase stage with live cubic coefficient interpolation
@@ -50,6 +69,7 @@ struct PolyDev {
 
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
                       hipStream_t stream);
 // dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.

@@ -2,6 +2,8 @@
 #include "gar_plan.hpp"
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <numeric>
 
 namespace gar {
@@ -85,7 +87,7 @@ inline void macroRow(const FirPeriodic& f, int r, int64_t& off, const std::vecto
     row = &f.rows[rr];
 }
 
-std::vector<RbGeom> geomFor(const FirPeriodic& f, int mp, double& eff) {
+std::vector<RbGeom> geomFor(const FirPeriodic& f, int mp, double& eff, int kstep = 4, int kalign = 4) {
     const int Pc = f.P * mp;
     const int nrb = (Pc + 15) / 16;
     std::vector<RbGeom> g(nrb);
@@ -102,10 +104,10 @@ std::vector<RbGeom> geomFor(const FirPeriodic& f, int mp, double& eff) {
             hi = std::max<int64_t>(hi, off + static_cast<int64_t>(row->size()));
             useful += static_cast<double>(row->size());
         }
-        const int64_t klo = (lo / 4) * 4;
+        const int64_t klo = (lo / kalign) * kalign;
         g[rb].klo = static_cast<int>(klo);
-        g[rb].nsteps = static_cast<int>((hi - klo + 3) / 4);
-        executed += 64.0 * g[rb].nsteps;
+        g[rb].nsteps = static_cast<int>((hi - klo + kstep - 1) / kstep);
+        executed += 16.0 * kstep * g[rb].nsteps;
     }
     eff = useful / executed;
     return g;
@@ -116,7 +118,7 @@ namespace {
 // Even split of the row blocks' steps over nprog programs (<= kBgMaxSeg
 // segments each); row blocks cut across programs get LDS slots + a reduction.
 bool splitPrograms(const std::vector<RbGeom>& rbs, int nprog, std::vector<BgProg>& progs, std::vector<BgRed>& reds,
-                   int& nslots, int& maxLen) {
+                   int& nslots, int& maxLen, int kstep = 4) {
     int64_t S = 0;
     for (const auto& r : rbs) S += r.nsteps;
     const int T = static_cast<int>((S + nprog - 1) / nprog);
@@ -133,7 +135,7 @@ bool splitPrograms(const std::vector<RbGeom>& rbs, int nprog, std::vector<BgProg
             const int take = std::min(rem, T - pg.len);
             BgSeg& sg = pg.seg[pg.nseg];
             sg.rb = static_cast<int>(rb);
-            sg.k0 = rbs[rb].klo + 4 * pos;
+            sg.k0 = rbs[rb].klo + kstep * pos;
             sg.ns = take;
             sg.start = pg.len;
             owners[rb].push_back({w, pg.nseg});
@@ -283,6 +285,158 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     plan.usefulMacsPerOutput = useful / f.P;
     double exec = 0;
     for (const auto& r : rbs) exec += 16.0 * 4.0 * r.nsteps;  // per column per macro period
+    plan.mfmaMacsPerOutput = exec / plan.Pc;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Split-f16 plan
+// ---------------------------------------------------------------------------
+std::vector<int> HxPlan::progTable() const {
+    std::vector<int> t(progs.size() * kBgProgInts, 0);
+    for (size_t i = 0; i < progs.size(); ++i) {
+        int* e = &t[i * kBgProgInts];
+        const BgProg& pg = progs[i];
+        e[0] = pg.nseg;
+        e[1] = pg.nseg >= 2 ? pg.seg[1].start : 1 << 20;
+        e[2] = pg.nseg >= 3 ? pg.seg[2].start : 1 << 20;
+        for (int j = 0; j < kBgMaxSeg; ++j) {
+            const BgSeg& sg = pg.seg[j];
+            e[3 + 4 * j] = sg.rb;
+            e[4 + 4 * j] = sg.k0 - kHxStep * sg.start;  // input row of step s = this + 32*s
+            e[5 + 4 * j] = sg.slot;
+            e[6 + 4 * j] = 0;
+        }
+    }
+    return t;
+}
+
+std::vector<int> HxPlan::redTable() const {
+    std::vector<int> t(reds.size() * kBgRedInts, 0);
+    for (size_t i = 0; i < reds.size(); ++i) {
+        int* e = &t[i * kBgRedInts];
+        e[0] = reds[i].rb;
+        e[1] = reds[i].n;
+        for (int k = 0; k < reds[i].n; ++k) e[2 + k] = reds[i].slot[k];
+    }
+    return t;
+}
+
+static uint16_t f16bits(double v) {
+    const _Float16 h = static_cast<_Float16>(v);
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+
+bool buildHxPlan(const FirPeriodic& f, HxPlan& plan) {
+    if (f.P <= 0 || f.Q <= 0) return false;
+    int bestMp = 1;
+    double bestEff = -1;
+    for (int mp = 1; mp <= 64; ++mp) {
+        const int Pc = f.P * mp;
+        if (Pc > 320) break;
+        double eff;
+        geomFor(f, mp, eff, kHxStep, 1);
+        if (Pc < 16) eff *= static_cast<double>(Pc) / 16.0;
+        if (eff > bestEff + 1e-9) { bestEff = eff; bestMp = mp; }
+    }
+    double eff;
+    const std::vector<RbGeom> rbs = geomFor(f, bestMp, eff, kHxStep, 1);
+    plan = HxPlan();
+    plan.P = f.P; plan.Q = f.Q; plan.mp = bestMp;
+    plan.Pc = f.P * bestMp;
+    plan.Qc = f.Q * bestMp;
+    plan.nrb = static_cast<int>(rbs.size());
+    for (const auto& r : rbs) plan.Kc = std::max(plan.Kc, r.klo + kHxStep * r.nsteps);
+
+    int maxLen = 0;
+    for (const auto& r : rbs) maxLen = std::max(maxLen, r.nsteps);
+    if (plan.nrb <= kHxRbMaxWaves && maxLen <= kHxRbMaxNS) {
+        // row-block mode: wave w runs row block w over its whole band
+        plan.rbMode = true;
+        plan.nw = plan.nrb;
+        plan.progs.assign(plan.nw, BgProg());
+        for (int w = 0; w < plan.nw; ++w) {
+            BgProg& pg = plan.progs[w];
+            pg.nseg = 1;
+            pg.len = rbs[w].nsteps;
+            pg.seg[0].rb = w;
+            pg.seg[0].k0 = rbs[w].klo;
+            pg.seg[0].ns = rbs[w].nsteps;
+        }
+        plan.kch = 1;
+        plan.NS = maxLen;
+        // waves 0..7 also stage the 8 column pairs of every block: pad with idle programs
+        while (static_cast<int>(plan.progs.size()) < 8) plan.progs.push_back(BgProg());
+    } else {
+        plan.nw = kHxWaves;
+        if (!splitPrograms(rbs, plan.nw, plan.progs, plan.reds, plan.nslots, maxLen, kHxStep)) return false;
+        plan.kch = (maxLen + kHxMaxNS - 1) / kHxMaxNS;
+        plan.NS = std::max(2, ((maxLen + plan.kch - 1) / plan.kch + 1) / 2 * 2);
+        if (plan.NS > kHxMaxNS) return false;
+    }
+
+    double amax = 0;
+    for (const auto& r : f.rows)
+        for (double v : r) amax = std::max(amax, std::fabs(v));
+    int ex = 0;
+    if (amax > 0) std::frexp(amax, &ex);
+    plan.ea = amax > 0 ? 15 - ex : 0;
+    const double sc = std::ldexp(1.0, plan.ea);
+
+    const int plen = plan.kch * plan.NS;
+    const int nprog = static_cast<int>(plan.progs.size());
+    plan.A.assign(static_cast<size_t>(nprog) * plen * 2 * 64 * 8, 0);
+    plan.Kread = plan.Kc;
+    for (int pi = 0; pi < nprog; ++pi) {
+        const BgProg& pg = plan.progs[pi];
+        for (int j = 0; j < pg.nseg; ++j) {
+            const BgSeg& sg = pg.seg[j];
+            const int runLen = j == pg.nseg - 1 ? plen - sg.start : sg.ns;
+            plan.Kread = std::max(plan.Kread, sg.k0 + kHxStep * runLen);
+            for (int s = 0; s < sg.ns; ++s)
+                for (int lane = 0; lane < 64; ++lane) {
+                    const int m = lane & 15, g = lane >> 4;
+                    const int r = sg.rb * 16 + m;
+                    if (r >= plan.Pc) continue;
+                    int64_t off;
+                    const std::vector<double>* row;
+                    macroRow(f, r, off, row);
+                    const size_t base = ((static_cast<size_t>(pi) * plen + sg.start + s) * 2 * 64 + lane) * 8;
+                    for (int jj = 0; jj < 8; ++jj) {
+                        const int64_t idx = sg.k0 + kHxStep * s + hxPermK(g, jj) - off;
+                        if (idx < 0 || idx >= static_cast<int64_t>(row->size())) continue;
+                        const double v = (*row)[idx] * sc;
+                        const uint16_t hb = f16bits(v);
+                        _Float16 hh;
+                        std::memcpy(&hh, &hb, 2);
+                        plan.A[base + jj] = hb;
+                        plan.A[base + 64 * 8 + jj] = f16bits(v - static_cast<double>(hh));
+                    }
+                }
+        }
+    }
+
+    plan.rowMax = 0;
+    for (const auto& r : f.rows) plan.rowMax = std::max(plan.rowMax, static_cast<int>(r.size()));
+    plan.rows.assign(static_cast<size_t>(plan.Pc) * plan.rowMax, 0.f);
+    plan.rowOff.assign(plan.Pc, 0);
+    plan.rowLen.assign(plan.Pc, 0);
+    for (int r = 0; r < plan.Pc; ++r) {
+        int64_t off;
+        const std::vector<double>* row;
+        macroRow(f, r, off, row);
+        plan.rowOff[r] = static_cast<int>(off);
+        plan.rowLen[r] = static_cast<int>(row->size());
+        for (size_t k = 0; k < row->size(); ++k) plan.rows[static_cast<size_t>(r) * plan.rowMax + k] = static_cast<float>((*row)[k]);
+    }
+
+    double useful = 0;
+    for (const auto& r : f.rows) useful += static_cast<double>(r.size());
+    plan.usefulMacsPerOutput = useful / f.P;
+    double exec = 0;
+    for (const auto& r : rbs) exec += 16.0 * kHxStep * r.nsteps;
     plan.mfmaMacsPerOutput = exec / plan.Pc;
     return true;
 }

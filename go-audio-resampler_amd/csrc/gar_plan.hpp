@@ -78,4 +78,46 @@ struct BgPlan {
 // Builds the MFMA plan (macro period, balanced wave programs, A image).
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
 
+// ---------------------------------------------------------------------------
+// Split-f16 plan (gar_hx.hpp): the same banded GEMM on
+// v_mfma_f32_16x16x32_f16 with every operand split into two f16 halves
+// (x = xh + xl, a = ah + al, both power-of-two scaled) and the three
+// products ah*xh + ah*xl + al*xh accumulated in f32.  One program step =
+// one 32-deep K slice of one row block = 3 MFMAs.  Within a slice, lane
+// group g (lanes 16g..16g+15) holds the inputs k0 + 4g + j (j < 4) and
+// k0 + 16 + 4g + (j - 4) (j >= 4), which is what two ds_read_b64_tr_b16 of
+// a [row][16 columns] f16 image deliver conflict-free; A is laid out in the
+// same permuted K order.
+// ---------------------------------------------------------------------------
+constexpr int kHxStep = 32;        // K per program step
+constexpr int kHxWaves = 8;        // segmented mode: compute waves per workgroup
+constexpr int kHxProducers = 4;    // + producer waves (one per SIMD)
+constexpr int kHxMaxNS = 12;       // segmented mode register budget: 8 VGPRs of A per step
+constexpr int kHxRbMaxWaves = 12;  // row-block mode: one compute wave per row block (<= 12 + 4 waves)
+constexpr int kHxRbMaxNS = 10;     // row-block mode register budget (1024-thread workgroup: 128 VGPRs)
+constexpr int kHxMaxRows = 1024;   // producer register staging: 16 rows per lane
+inline int hxPermK(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
+
+struct HxPlan {
+    int P = 0, Q = 0, mp = 1;
+    int Pc = 0, Qc = 0, nrb = 0;
+    int Kc = 0;                       // rows of a macro period's window holding input the band reads
+    int Kread = 0;                    // rows the padded program steps read (>= Kc)
+    int NS = 0, kch = 1, nw = kHxWaves, nslots = 0;
+    bool rbMode = false;              // one row block per compute wave: no segments, no partial sums
+    int ea = 0;                       // coefficient scale: A * 2^ea has max |.| in [2^14, 2^15)
+    std::vector<BgProg> progs;        // [nw]; BgSeg::k0 = first input row of the segment
+    std::vector<BgRed> reds;
+    std::vector<uint16_t> A;          // [nw][kch*NS][2 (hi, lo)][64 lanes][8] f16 bits
+    int rowMax = 0;                   // non-finite fallback: f32 rows [Pc][rowMax], offsets, lengths
+    std::vector<float> rows;
+    std::vector<int> rowOff, rowLen;
+    double usefulMacsPerOutput = 0;
+    double mfmaMacsPerOutput = 0;     // executed MACs (one of the three products) per output
+    std::vector<int> progTable() const;  // [nw][kBgProgInts]
+    std::vector<int> redTable() const;
+};
+
+bool buildHxPlan(const FirPeriodic& f, HxPlan& plan);
+
 }  // namespace gar

@@ -19,7 +19,7 @@ QualityQuick, QualityLow, QualityMedium, QualityHigh, QualityVeryHigh, QualityCu
 # engine.Quality (internal/engine/filter_params.go:16-41)
 (EngineQuick, EngineLow, EngineMedium, EngineHigh, EngineVeryHigh,
  Engine16Bit, Engine20Bit, Engine24Bit, Engine28Bit, Engine32Bit) = range(10)
-F64, F32 = 0, 1
+F64, F32, F32_EXACT = 0, 1, 2
 
 GAR_OK, INVALID_CONFIG, BUFFER_TOO_SMALL, NOT_SUPPORTED, CHANNEL_MISMATCH, DEVICE, INTERNAL, INVALID_ARGUMENT = range(8)
 
@@ -102,6 +102,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libgar.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    # One HIP runtime per process: libgar.so and torch both depend on the
+    # soname libamdhip64.so.7, and whichever is loaded first serves both.  Load
+    # torch's first (it carries its own libhsa-runtime64) so the two stay in
+    # step; the standalone C ABI (cgo) simply uses the system ROCm.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32, i64, d, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.POINTER(C.c_double)
     sig = {

@@ -44,8 +44,10 @@ enum { GAR_QUALITY_QUICK = 0, GAR_QUALITY_LOW = 1, GAR_QUALITY_MEDIUM = 2, GAR_Q
 /* resampler.QualityFlags (resample.go:133-153) */
 enum { GAR_FLAG_NO_INTERPOLATION = 1, GAR_FLAG_MINIMUM_PHASE = 2, GAR_FLAG_LINEAR_PHASE = 4,
        GAR_FLAG_ALLOW_ALIASING = 8, GAR_FLAG_NO_SIMD = 16 };
-/* sample / compute types */
-enum { GAR_F64 = 0, GAR_F32 = 1 };
+/* sample / compute types.  Compute: GAR_F64 (the reference's float64), GAR_F32 (float32-class:
+ * f16-split products on the f16 matrix cores, f32 accumulation, error <= exact-f32 arithmetic's),
+ * GAR_F32_EXACT (exact f32 products on the f32 matrix cores). */
+enum { GAR_F64 = 0, GAR_F32 = 1, GAR_F32_EXACT = 2 };
 /* engine.Quality (internal/engine/filter_params.go:16-41), for gar_design_engine */
 enum { GAR_ENGINE_QUICK = 0, GAR_ENGINE_LOW, GAR_ENGINE_MEDIUM, GAR_ENGINE_HIGH, GAR_ENGINE_VERYHIGH,
        GAR_ENGINE_16BIT, GAR_ENGINE_20BIT, GAR_ENGINE_24BIT, GAR_ENGINE_28BIT, GAR_ENGINE_32BIT };
@@ -70,7 +72,7 @@ typedef struct gar_config {
     int32_t enable_simd;
     int32_t enable_parallel;
     /* extensions (zero = reference behaviour) */
-    int32_t compute_dtype; /* GAR_F64 (the New path computes in float64, constant.go:121-146) or GAR_F32 */
+    int32_t compute_dtype; /* GAR_F64 (the New path computes in float64, constant.go:121-146), GAR_F32, GAR_F32_EXACT */
     int32_t device;        /* HIP device ordinal */
     int32_t dry_run;       /* 1: host state machine only, no GPU work; process calls report lengths only */
 } gar_config;

@@ -1,0 +1,116 @@
+"""GPU: the float32 compute path (split-f16 MFMA kernel, csrc/gar_hx.hpp) against
+the oracle and against the exact-f32 MFMA kernel (GAR_F32_EXACT).
+
+Tolerances: BASELINE.json north_star float32 <= 1e-6 RMS vs the reference.
+The split path's error must also stay within 2x of exact-f32 arithmetic's
+(it is in fact below it: 22-bit operands, f32 accumulation).
+Edge cases: Inf/NaN blocks (IEEE propagation via the in-kernel f32 fallback),
+extreme magnitudes (power-of-two block scaling), ragged lengths, both
+directions, the DFT-only / decimator stages and chunked streaming.
+"""
+import numpy as np
+import pytest
+
+from helpers import F32_RMS_TOL, chunk_sizes, oracle_new, rms, signal
+
+pytestmark = pytest.mark.gpu
+
+
+def run(gar, torch, in_rate, out_rate, x, preset, dtype, chunks=None):
+    ch = x.shape[1]
+    r = gar.New(gar.Config(in_rate, out_rate, ch, preset, ComputeDtype=dtype))
+    xd = torch.from_numpy(np.ascontiguousarray(x)).float().cuda()
+    outs, s = [], 0
+    for n in (chunks or [x.shape[0]]):
+        outs.append(r.process_device(xd[s:s + n]).clone())
+        s += n
+    outs.append(r.flush_device(dtype=torch.float32).clone())
+    torch.cuda.synchronize()
+    return torch.cat(outs).double().cpu().numpy()
+
+
+CASES = [
+    (44100, 48000, 2, "QualityHigh"),      # cfg2 geometry (fused composite)
+    (48000, 44100, 5, "QualityVeryHigh"),  # cfg3 geometry, odd channel count
+    (96000, 44100, 3, "QualityVeryHigh"),  # decimator + fused
+    (22050, 44100, 1, "QualityHigh"),      # DFT-only (integer up)
+    (48000, 16000, 2, "QualityMedium"),    # integer down (decimator)
+    (44100, 96000, 4, "QualityLow"),       # halfband x2 + fused
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_hx_vs_oracle_and_exact(gar, O, cuda, case):
+    ir, orr, ch, q = case
+    n = 30011  # ragged
+    x = signal(n, ch, ir, seed=ir + ch).astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, ir, orr, x, getattr(gar, q), gar.F32)
+    ex = run(gar, cuda, ir, orr, x, getattr(gar, q), gar.F32_EXACT)
+    want = oracle_new(O, ir, orr, x, getattr(O, "P_" + q[7:].upper()))
+    for c in range(ch):
+        assert got.shape[0] == ex.shape[0] == len(want[c])
+        e_hx, e_ex = rms(got[:, c], want[c]), rms(ex[:, c], want[c])
+        assert e_hx <= F32_RMS_TOL, e_hx
+        assert e_hx <= max(2.0 * e_ex, 1e-8), (e_hx, e_ex)
+
+
+@pytest.mark.parametrize("chunk", [4096, 1001])
+def test_hx_chunked_equals_oracle(gar, O, cuda, chunk):
+    x = signal(50000, 2, 44100).astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32, chunk_sizes(50000, chunk))
+    want = oracle_new(O, 44100, 48000, x, O.P_HIGH)
+    for c in range(2):
+        assert got.shape[0] == len(want[c])
+        assert rms(got[:, c], want[c]) <= F32_RMS_TOL
+
+
+@pytest.mark.parametrize("scale", [1e30, 1e-30, 3.0e4])
+def test_hx_extreme_magnitudes(gar, O, cuda, scale):
+    """Block power-of-two scaling: error stays relative to the signal level."""
+    x = signal(40000, 2, 44100, seed=7)
+    xs = (x * scale).astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 44100, 48000, xs, gar.QualityHigh, gar.F32)
+    want = oracle_new(O, 44100, 48000, xs, O.P_HIGH)
+    for c in range(2):
+        assert np.all(np.isfinite(got[:, c]))
+        assert rms(got[:, c] / scale, want[c] / scale) <= F32_RMS_TOL
+
+
+def test_hx_mixed_levels(gar, O, cuda):
+    """A loud channel beside a very quiet one (per-quad scales differ)."""
+    x = signal(40000, 2, 44100, seed=9)
+    x[:, 1] *= 1e-6
+    x = x.astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
+    want = oracle_new(O, 44100, 48000, x, O.P_HIGH)
+    assert rms(got[:, 0], want[0]) <= F32_RMS_TOL
+    assert rms(got[:, 1] * 1e6, want[1] * 1e6) <= F32_RMS_TOL
+
+
+def test_hx_nonfinite_propagates(gar, O, cuda):
+    """Inf / NaN samples: every output the reference makes non-finite is
+    non-finite here too (blocks holding them take the in-kernel IEEE f32
+    fallback over the exact FIR rows); everything else matches the oracle."""
+    n = 60000
+    x = signal(n, 2, 44100, seed=11).astype(np.float32).astype(np.float64)
+    x[20000, 0] = np.inf
+    x[41000, 1] = np.nan
+    got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
+    want = oracle_new(O, 44100, 48000, x, O.P_HIGH)
+    for c in range(2):
+        w = np.asarray(want[c])
+        fin = np.isfinite(w)
+        assert not fin.all()
+        bad = np.nonzero(np.isfinite(got[:, c]) != fin)[0]
+        assert bad.size == 0, (c, bad[:20], got[bad[:5], c], w[bad[:5]])
+        if c == 1:  # a NaN sample: NaN exactly where the reference has NaN
+            np.testing.assert_array_equal(np.isnan(got[:, c]), np.isnan(w))
+        # (an Inf sample: the fused single-stage FIR gives +-Inf where the two-stage
+        # reference sums +Inf and -Inf intermediates into NaN -- same non-finite set)
+        assert rms(got[fin, c], w[fin]) <= F32_RMS_TOL
+
+
+def test_hx_zero_input(gar, O, cuda):
+    x = np.zeros((20000, 2))
+    got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
+    assert np.all(got == 0.0)
