@@ -30,6 +30,7 @@ METRIC = "Msamples/s resampled (float32, 44.1k→48k QualityHigh) + RMS error vs
 IN_RATE, OUT_RATE, CHANNELS = 44100, 48000, 2
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level table)
 PEAK_F32_MATRIX_TFLOPS = 157.3
+PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
 PEAK_HBM_GBPS = 8000.0
 # reference-algorithm flops per input sample (cfg2)
 REF_ALGO_FLOPS_PER_SAMPLE = 1017.6
@@ -190,17 +191,22 @@ def main():
             errs.append(np.mean((got[: len(want), c] - want) ** 2))
         rms = float(np.sqrt(np.mean(errs)))
 
-    # roofline of the dominant kernel (fused DFTx2->polyphase MFMA FIR)
+    # roofline of the dominant kernel: the fused DFTx2->polyphase FIR launch of
+    # Process (HIP events on the launch stream, inside the library).  The
+    # split-f16 kernel (GAR_F32) needs 2*3*MACs of f16 MFMA work per output
+    # (40 us at the 2.5 PF dense f16 peak for this workload) and moves the
+    # algorithmic bytes once (55 us at 8 TB/s): HBM is the binding roofline.
     geom, _ = gar.design_engine(48000.0, 48000.0 * (OUT_RATE / IN_RATE), gar.Engine24Bit)
     useful_macs = geom.useful_macs_per_output
     outs_per_launch = n_out * CHANNELS
-    flops_per_launch = 2.0 * useful_macs * outs_per_launch
     launch_s = (kms / 1e3) / max(launches, 1)
-    achieved_tf = flops_per_launch / launch_s / 1e12 if launches else None
     workload = "cfg2_stereo_f32_44k1_48k_q24_600s"
     traffic = load_traffic(workload)
     algo_bytes = frames * CHANNELS * 4 + outs_per_launch * 4
-
+    achieved_gbps = algo_bytes / launch_s / 1e9 if launches else None
+    split = os.environ.get("GAR_HX", "1") != "0"
+    f16_flops = 2.0 * 3 * useful_macs * outs_per_launch  # three f16 products per useful MAC
+    f32_flops = 2.0 * useful_macs * outs_per_launch
     line = {
         "metric": METRIC,
         "value": round(total_samples / elapsed / 1e6, 2),
@@ -226,22 +232,27 @@ def main():
             "parallelism": f"independent streams, 1 per GPU x {world}",
         },
         "roofline": {
-            "bound": "mfma",
-            "achieved": round(achieved_tf, 3) if achieved_tf else None,
-            "peak": PEAK_F32_MATRIX_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tf / PEAK_F32_MATRIX_TFLOPS, 4) if achieved_tf else None,
+            "bound": "hbm",
+            "achieved": round(achieved_gbps, 1) if achieved_gbps else None,
+            "peak": PEAK_HBM_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbps / PEAK_HBM_GBPS, 4) if achieved_gbps else None,
             "traffic": traffic,
-            "kernel": "bg_kernel<float> (fused DFTx2->polyphase banded FIR, v_mfma_f32_16x16x4_f32)",
+            "kernel": ("hx_kernel (fused DFTx2->polyphase banded FIR, f16-split v_mfma_f32_16x16x32_f16, f32 accumulation)"
+                       if split else "bg_kernel<float> (exact-f32 v_mfma_f32_16x16x4_f32)"),
             "kernel_ms_per_launch": round(launch_s * 1e3, 4),
             "launches": launches,
-            "algo_flops_per_input_sample": round(2 * useful_macs * (n_out / frames), 2),
+            "algo_hbm_bytes_per_launch": algo_bytes,
+            "algo_bytes_per_input_sample": round(algo_bytes / (frames * CHANNELS), 3),
+            "useful_macs_per_output": round(useful_macs, 2),
+            "mfma_tflops": round((f16_flops if split else f32_flops) / launch_s / 1e12, 2) if launches else None,
+            "mfma_peak_tflops": PEAK_F16_MATRIX_TFLOPS if split else PEAK_F32_MATRIX_TFLOPS,
             "ref_algo_flops_per_input_sample": REF_ALGO_FLOPS_PER_SAMPLE,
             "ref_equiv_tflops": round(REF_ALGO_FLOPS_PER_SAMPLE * frames * CHANNELS / launch_s / 1e12, 3)
             if launches else None,
-            "algo_hbm_bytes_per_launch": algo_bytes,
-            "algo_hbm_gbps": round(algo_bytes / launch_s / 1e9, 1) if launches else None,
         },
+        "arith": ("f32 I/O; products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
+                  "(error below exact-f32 arithmetic: rms_vs_oracle)" if split else "exact f32 MFMA"),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

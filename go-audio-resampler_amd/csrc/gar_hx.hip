@@ -1,16 +1,19 @@
-// gar_hx.hip -- instantiations and launch geometry of the split-f16 FIR kernel (gar_hx.hpp).
+// gar_hx.hip -- launch geometry of the split-f16 FIR kernel (gar_hx.hpp): the
+// interior chunks of a launch run on hx_kernel, its edges on fir_kernel.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "gar_hx.hpp"
 
 namespace gar {
 
+namespace {
+
 template <int NS, bool RB>
-static hipError_t hxDispatch(const HxDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, size_t lds,
-                             int64_t blocks, hipStream_t st) {
+hipError_t hxDispatch(const HxArgs& x, int waves, size_t lds, int64_t blocks, hipStream_t st) {
     static bool attrSet = false;
     if (!attrSet) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, true>),
@@ -20,85 +23,162 @@ static hipError_t hxDispatch(const HxDev& p, const SrcDesc& src, const OutDesc& 
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attrSet = true;
     }
-    const int waves = RB ? std::max(p.nw, 8) : kHxWaves;
-    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * waves);
-    if (RB || p.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, RB, true>), gd, bd, lds, st, p, src, od, g, p.ea);
-    else hipLaunchKernelGGL((hx_kernel<NS, RB, false>), gd, bd, lds, st, p, src, od, g, p.ea);
+    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * (waves + 2));  // + 2 stager waves
+    if (RB || x.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, RB, true>), gd, bd, lds, st, x, waves);
+    else hipLaunchKernelGGL((hx_kernel<NS, RB, false>), gd, bd, lds, st, x, waves);
     return hipGetLastError();
 }
 
+hipError_t launchFir(const HxDev& p, const SrcDesc& src, OutDesc od, int64_t lo, int64_t hi, int C, hipStream_t st) {
+    if (hi <= lo) return hipSuccess;
+    od.o_lo = lo;
+    od.o_hi = hi;
+    const int64_t n = (hi - lo) * C;  // one wave per output
+    const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
+    hipLaunchKernelGGL(fir_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, src, od, C, p.Pc, p.Qc,
+                       p.rowOff, p.rowLen, p.rows, p.rowMax);
+    return hipGetLastError();
+}
+
+int64_t floorDiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+int64_t ceilDiv(int64_t a, int64_t b) { return -floorDiv(-a, b); }
+
+}  // namespace
+
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
-    // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bit 1 skips staging
-    // after the first block, bit 2 skips the MFMA programs (timing decomposition only)
+    // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bits: 1 skip
+    // staging after the first block, 2 skip the MFMA programs, 8 skip the fixup, 16 skip the loop
     static const int knobG = std::getenv("GAR_HX_G") ? std::atoi(std::getenv("GAR_HX_G")) : 0;
     static const int knobDbg = std::getenv("GAR_HX_DBG") ? std::atoi(std::getenv("GAR_HX_DBG")) : 0;
-    BgGrid g{};
-    g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;
-    g.nprog = p.nw; g.kch = p.kch; g.nwt = p.nw; g.ncg = 1;
-    g.nred = p.nred; g.nslots = p.nslots;
-    g.a_lo = od.o_lo / p.Pc;
-    const int64_t a_hi = (od.o_hi + p.Pc - 1) / p.Pc;
-    const int64_t nmac = a_hi - g.a_lo;
-    const size_t slotBytes = static_cast<size_t>(g.nslots) * 256 * 4;
+    const int64_t Pc = p.Pc, Qc = p.Qc;
+    const int64_t a_lo = od.o_lo / Pc;
+    const int64_t nmac = (od.o_hi + Pc - 1) / Pc - a_lo;
+    const size_t slotBytes = static_cast<size_t>(p.nslots) * 256 * 4;
     const size_t kLds = 160 * 1024;
-    auto wsFor = [&](int G) { return (p.Kread + (G - 1) * p.Qc + 63) / 64 * 64; };  // whole DMA row chunks
-    auto ldsFor = [&](int G, int par) { return 4 * static_cast<size_t>(wsFor(G)) * 32 + (par ? 2 : 1) * slotBytes + 128; };
-    g.parity = (g.nred > 0 && ldsFor(1, 1) <= kLds) ? 1 : 0;
+    // window rows staged per column: whole DMA row chunks, >= W + 1 (stereo frame pairs may
+    // start one row early)
+    auto wsFor = [&](int G) { return (p.Kread + (G - 1) * p.Qc + 1 + 127) / 128 * 128; };
+    // two buffers of 4 quads x (16*Ws + 64) B, partial slots, colExp + fixup flag
+    auto ldsFor = [&](int G, int par) {
+        return 8 * (16 * static_cast<size_t>(wsFor(G)) + 64) + (par ? 2 : 1) * slotBytes + 160;
+    };
+    const int parity = (p.nred > 0 && ldsFor(1, 1) <= kLds) ? 1 : 0;
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    // G macro periods per column: the largest whose window fits the producers'
-    // register staging and LDS without dropping below one block per CU (when
-    // the launch is large enough for that)
+    // G macro periods per column: the largest whose window fits LDS without
+    // dropping below one block per CU (when the launch is large enough for that)
     auto nbFor = [&](int G) { return ((nmac + G - 1) / G * C + 15) / 16; };
     int G = 1;
     for (int cand = 2; cand <= 8; ++cand) {
-        if (cand > nmac || wsFor(cand) > kHxMaxRows || ldsFor(cand, g.parity) > kLds) break;
+        if (cand > nmac || wsFor(cand) > kHxMaxRows || ldsFor(cand, parity) > kLds) break;
         if (nbFor(cand) < ncu && nbFor(1) >= ncu) break;
         G = cand;
     }
     if (knobG > 0 && knobG < G) G = knobG;
-    if (wsFor(G) > kHxMaxRows || ldsFor(G, g.parity) > kLds) return hipErrorInvalidConfiguration;
-    g.G = G;
-    g.W = p.Kc + (G - 1) * p.Qc;
-    g.Wl = p.Kread + (G - 1) * p.Qc;
-    g.Ws = wsFor(G);
-    const int64_t nchunk = (nmac + G - 1) / G;
-    g.nchunk = static_cast<int>(nchunk);
-    g.ncols = static_cast<int>(nchunk * C);
-    g.nblocks = (g.ncols + 15) / 16;
-    g.dbg = knobDbg;
-    g.vst = 0;
-    if (!od.f64) {
-        if (od.fs == 1) g.vst = 1;
-        else if (C == 2 && od.fs == 2 && od.cs == 1) g.vst = 2;
+    const int64_t W = p.Kc + static_cast<int64_t>(G - 1) * Qc;
+
+    // interior chunks [k0, k1): outputs inside [o_lo, o_hi), window (+1 row, see wsFor)
+    // inside the f32 input; a stereo window may also reach one frame before its start
+    int64_t k0 = 0, k1 = 0;
+    if (src.in && !src.in_f64 && src.in_len > 0 && wsFor(G) <= kHxMaxRows && ldsFor(G, parity) <= kLds) {
+        const int64_t GQ = G * Qc, GP = G * Pc;
+        const int64_t inEnd = std::min(src.in_base + src.in_len, src.valid_end);
+        k0 = std::max<int64_t>({0, ceilDiv(od.o_lo - a_lo * Pc, GP), ceilDiv(src.in_base + 1 - a_lo * Qc, GQ)});
+        k1 = std::min<int64_t>(floorDiv(od.o_hi - a_lo * Pc, GP), floorDiv(inEnd - W - 1 - a_lo * Qc, GQ) + 1);
     }
-    if (g.nblocks <= 0) return hipSuccess;
-    const size_t lds = ldsFor(G, g.parity);
-    const int64_t blocks = std::min<int64_t>(g.nblocks, ncu);
+    const int64_t ncols = (k1 - k0) * C;
+    static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
+    if (trace)
+        fprintf(stderr, "hx: o[%lld,%lld) C=%d G=%d W=%lld a_lo=%lld k0=%lld k1=%lld in_base=%lld in_len=%lld valid_end=%lld hist_len=%lld\n",
+                (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)W, (long long)a_lo, (long long)k0, (long long)k1,
+                (long long)src.in_base, (long long)src.in_len, (long long)src.valid_end, (long long)src.hist_len);
+    if (ncols < 64 || ncols > (int64_t(1) << 30)) return launchFir(p, src, od, od.o_lo, od.o_hi, C, stream);
+
+    HxArgs x{};
+    x.A = static_cast<const h8v*>(p.A);
+    x.progs = p.progs;
+    x.reds = p.reds;
+    x.fix = p.fix;
+    x.fixCap = p.fixCap;
+    x.ea = p.ea;
+    x.kch = p.kch;
+    x.Pc = p.Pc; x.Qc = p.Qc; x.G = G; x.C = C;
+    x.W = static_cast<int>(W);
+    x.Ws = wsFor(G);
+    x.ncols = static_cast<int>(ncols);
+    x.nblocks = static_cast<int>((ncols + 15) / 16);
+    x.nred = p.nred; x.nslots = p.nslots; x.parity = parity;
+    x.dbg = knobDbg;
+    x.a0 = a_lo + k0 * G;
+    const float* in = static_cast<const float*>(src.in);
+    x.in = in + (x.a0 * Qc - src.in_base) * src.in_fs;
+    x.in_fs = src.in_fs;
+    x.in_cs = src.in_cs;
+    x.in_chunk = G * Qc * src.in_fs;
+    const int esz = od.f64 ? 8 : 4;
+    x.out_f64 = od.f64;
+    x.out = static_cast<char*>(od.out) + (x.a0 * Pc - od.o0) * od.fs * esz;
+    x.out_fs = od.fs * esz;
+    x.out_cs = od.cs * esz;
+    x.out_chunk = G * Pc * od.fs * esz;
+    // epilogue layout (16-B stores need every row quad 16-B aligned)
+    const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
+    if (od.f64) x.vst = 3;
+    else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 2 == 0) x.vst = 2;
+    else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;
+    else x.vst = 0;
+    // raw staging format: 16-B LDS-DMA pieces where the layout allows it
+    const bool inAl = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+    x.fmt = 0;
+    if (inAl && C == 2 && src.in_fs == 2 && src.in_cs == 1) {
+        x.fmt = 1;
+        x.par0 = static_cast<int>((x.a0 * Qc - src.in_base) & 1);
+        x.gqOdd = static_cast<int>((G * Qc) & 1);
+    } else if (inAl && C % 4 == 0 && src.in_cs == 1 && (src.in_fs * 4) % 16 == 0) {
+        x.fmt = 2;
+    }
+    static const bool noFmt = std::getenv("GAR_HX_DWORD") != nullptr;
+    if (noFmt) x.fmt = 0;
+    x.src = src;
+    x.od = od;
+    x.rows = p.rows;
+    x.rowOff = p.rowOff;
+    x.rowLen = p.rowLen;
+    x.rowMax = p.rowMax;
+    x.zero = p.zero;
+
+    // edges first (they run while nothing else is queued), then the interior
+    hipError_t e = launchFir(p, src, od, od.o_lo, x.a0 * Pc, C, stream);
+    if (e != hipSuccess) return e;
+    e = launchFir(p, src, od, (a_lo + k1 * G) * Pc, od.o_hi, C, stream);
+    if (e != hipSuccess) return e;
+
+    const size_t lds = ldsFor(G, parity);
+    const int64_t blocks = std::min<int64_t>(x.nblocks, ncu);
     if (p.rb) {
         if (p.nw > kHxRbMaxWaves) return hipErrorInvalidConfiguration;
+        const int waves = p.nw;
         switch (p.NS) {
-            case 1: return hxDispatch<1, true>(p, src, od, g, lds, blocks, stream);
-            case 2: return hxDispatch<2, true>(p, src, od, g, lds, blocks, stream);
-            case 3: return hxDispatch<3, true>(p, src, od, g, lds, blocks, stream);
-            case 4: return hxDispatch<4, true>(p, src, od, g, lds, blocks, stream);
-            case 5: return hxDispatch<5, true>(p, src, od, g, lds, blocks, stream);
-            case 6: return hxDispatch<6, true>(p, src, od, g, lds, blocks, stream);
-            case 7: return hxDispatch<7, true>(p, src, od, g, lds, blocks, stream);
-            case 8: return hxDispatch<8, true>(p, src, od, g, lds, blocks, stream);
-            case 9: return hxDispatch<9, true>(p, src, od, g, lds, blocks, stream);
-            case 10: return hxDispatch<10, true>(p, src, od, g, lds, blocks, stream);
+            case 1: return hxDispatch<1, true>(x, waves, lds, blocks, stream);
+            case 2: return hxDispatch<2, true>(x, waves, lds, blocks, stream);
+            case 3: return hxDispatch<3, true>(x, waves, lds, blocks, stream);
+            case 4: return hxDispatch<4, true>(x, waves, lds, blocks, stream);
+            case 5: return hxDispatch<5, true>(x, waves, lds, blocks, stream);
+            case 6: return hxDispatch<6, true>(x, waves, lds, blocks, stream);
+            case 7: return hxDispatch<7, true>(x, waves, lds, blocks, stream);
+            case 8: return hxDispatch<8, true>(x, waves, lds, blocks, stream);
+            case 9: return hxDispatch<9, true>(x, waves, lds, blocks, stream);
+            case 10: return hxDispatch<10, true>(x, waves, lds, blocks, stream);
             default: return hipErrorInvalidConfiguration;
         }
     }
     switch (p.NS) {
-        case 2: return hxDispatch<2, false>(p, src, od, g, lds, blocks, stream);
-        case 4: return hxDispatch<4, false>(p, src, od, g, lds, blocks, stream);
-        case 6: return hxDispatch<6, false>(p, src, od, g, lds, blocks, stream);
-        case 8: return hxDispatch<8, false>(p, src, od, g, lds, blocks, stream);
-        case 10: return hxDispatch<10, false>(p, src, od, g, lds, blocks, stream);
-        case 12: return hxDispatch<12, false>(p, src, od, g, lds, blocks, stream);
+        case 2: return hxDispatch<2, false>(x, kHxWaves, lds, blocks, stream);
+        case 4: return hxDispatch<4, false>(x, kHxWaves, lds, blocks, stream);
+        case 6: return hxDispatch<6, false>(x, kHxWaves, lds, blocks, stream);
+        case 8: return hxDispatch<8, false>(x, kHxWaves, lds, blocks, stream);
+        case 10: return hxDispatch<10, false>(x, kHxWaves, lds, blocks, stream);
         default: return hipErrorInvalidConfiguration;
     }
 }

@@ -367,8 +367,6 @@ bool buildHxPlan(const FirPeriodic& f, HxPlan& plan) {
         }
         plan.kch = 1;
         plan.NS = maxLen;
-        // waves 0..7 also stage the 8 column pairs of every block: pad with idle programs
-        while (static_cast<int>(plan.progs.size()) < 8) plan.progs.push_back(BgProg());
     } else {
         plan.nw = kHxWaves;
         if (!splitPrograms(rbs, plan.nw, plan.progs, plan.reds, plan.nslots, maxLen, kHxStep)) return false;

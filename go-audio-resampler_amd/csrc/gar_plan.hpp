@@ -90,12 +90,11 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
 // same permuted K order.
 // ---------------------------------------------------------------------------
 constexpr int kHxStep = 32;        // K per program step
-constexpr int kHxWaves = 8;        // segmented mode: compute waves per workgroup
-constexpr int kHxProducers = 4;    // + producer waves (one per SIMD)
-constexpr int kHxMaxNS = 12;       // segmented mode register budget: 8 VGPRs of A per step
-constexpr int kHxRbMaxWaves = 12;  // row-block mode: one compute wave per row block (<= 12 + 4 waves)
-constexpr int kHxRbMaxNS = 10;     // row-block mode register budget (1024-thread workgroup: 128 VGPRs)
-constexpr int kHxMaxRows = 1024;   // producer register staging: 16 rows per lane
+constexpr int kHxWaves = 8;        // segmented mode: compute waves per workgroup (+ 2 stager waves)
+constexpr int kHxMaxNS = 10;       // segmented mode register budget: 8 VGPRs of A per step (10 waves: 168 VGPRs)
+constexpr int kHxRbMaxWaves = 10;  // row-block mode: one compute wave per row block (+ 2 stagers: 3 waves/SIMD)
+constexpr int kHxRbMaxNS = 10;     // row-block mode register budget (168 VGPRs)
+constexpr int kHxMaxRows = 1024;   // window rows per block: 16 per lane of a stager wave
 inline int hxPermK(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 struct HxPlan {
