@@ -18,14 +18,18 @@ hipError_t hxDispatch(const HxArgs& x, int waves, size_t lds, int64_t blocks, hi
     if (!attrSet) {
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, true>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (!RB)
+        if constexpr (!RB)
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, false>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attrSet = true;
     }
-    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * (waves + 2));  // + 2 stager waves
-    if (RB || x.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, RB, true>), gd, bd, lds, st, x, waves);
-    else hipLaunchKernelGGL((hx_kernel<NS, RB, false>), gd, bd, lds, st, x, waves);
+    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * waves);
+    if constexpr (RB) {
+        hipLaunchKernelGGL((hx_kernel<NS, true, true>), gd, bd, lds, st, x);
+    } else {
+        if (x.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, false, true>), gd, bd, lds, st, x);
+        else hipLaunchKernelGGL((hx_kernel<NS, false, false>), gd, bd, lds, st, x);
+    }
     return hipGetLastError();
 }
 
@@ -48,7 +52,8 @@ int64_t ceilDiv(int64_t a, int64_t b) { return -floorDiv(-a, b); }
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bits: 1 skip
-    // staging after the first block, 2 skip the MFMA programs, 8 skip the fixup, 16 skip the loop
+    // staging after the first block, 2 skip the MFMA programs, 8 skip the fixup, 16 skip the loop,
+    // 32 skip the f16 conversion, 64 skip the LDS-DMA
     static const int knobG = std::getenv("GAR_HX_G") ? std::atoi(std::getenv("GAR_HX_G")) : 0;
     static const int knobDbg = std::getenv("GAR_HX_DBG") ? std::atoi(std::getenv("GAR_HX_DBG")) : 0;
     const int64_t Pc = p.Pc, Qc = p.Qc;
@@ -56,10 +61,10 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     const int64_t nmac = (od.o_hi + Pc - 1) / Pc - a_lo;
     const size_t slotBytes = static_cast<size_t>(p.nslots) * 256 * 4;
     const size_t kLds = 160 * 1024;
-    // window rows staged per column: whole DMA row chunks, >= W + 1 (stereo frame pairs may
-    // start one row early)
-    auto wsFor = [&](int G) { return (p.Kread + (G - 1) * p.Qc + 1 + 127) / 128 * 128; };
-    // two buffers of 4 quads x (16*Ws + 64) B, partial slots, colExp + fixup flag
+    // window rows staged per column (the padded program steps read up to Kread + (G-1)*Qc),
+    // whole 64-row item slots
+    auto wsFor = [&](int G) { return (p.Kread + (G - 1) * p.Qc + 63) / 64 * 64; };
+    // two buffers of 4 quads x (16*Ws + 64) B, partial slots, quad exponent sets + fixup flag
     auto ldsFor = [&](int G, int par) {
         return 8 * (16 * static_cast<size_t>(wsFor(G)) + 64) + (par ? 2 : 1) * slotBytes + 160;
     };
@@ -78,14 +83,13 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     if (knobG > 0 && knobG < G) G = knobG;
     const int64_t W = p.Kc + static_cast<int64_t>(G - 1) * Qc;
 
-    // interior chunks [k0, k1): outputs inside [o_lo, o_hi), window (+1 row, see wsFor)
-    // inside the f32 input; a stereo window may also reach one frame before its start
+    // interior chunks [k0, k1): outputs inside [o_lo, o_hi), window rows [0, W) inside the f32 input
     int64_t k0 = 0, k1 = 0;
     if (src.in && !src.in_f64 && src.in_len > 0 && wsFor(G) <= kHxMaxRows && ldsFor(G, parity) <= kLds) {
         const int64_t GQ = G * Qc, GP = G * Pc;
         const int64_t inEnd = std::min(src.in_base + src.in_len, src.valid_end);
-        k0 = std::max<int64_t>({0, ceilDiv(od.o_lo - a_lo * Pc, GP), ceilDiv(src.in_base + 1 - a_lo * Qc, GQ)});
-        k1 = std::min<int64_t>(floorDiv(od.o_hi - a_lo * Pc, GP), floorDiv(inEnd - W - 1 - a_lo * Qc, GQ) + 1);
+        k0 = std::max<int64_t>({0, ceilDiv(od.o_lo - a_lo * Pc, GP), ceilDiv(src.in_base - a_lo * Qc, GQ)});
+        k1 = std::min<int64_t>(floorDiv(od.o_hi - a_lo * Pc, GP), floorDiv(inEnd - W - a_lo * Qc, GQ) + 1);
     }
     const int64_t ncols = (k1 - k0) * C;
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
@@ -128,16 +132,11 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 2 == 0) x.vst = 2;
     else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;
     else x.vst = 0;
-    // raw staging format: 16-B LDS-DMA pieces where the layout allows it
-    const bool inAl = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
+    // raw load format: 8-B stereo frames / 16-B four-channel rows where the layout allows it
+    const uintptr_t inA = reinterpret_cast<uintptr_t>(in);
     x.fmt = 0;
-    if (inAl && C == 2 && src.in_fs == 2 && src.in_cs == 1) {
-        x.fmt = 1;
-        x.par0 = static_cast<int>((x.a0 * Qc - src.in_base) & 1);
-        x.gqOdd = static_cast<int>((G * Qc) & 1);
-    } else if (inAl && C % 4 == 0 && src.in_cs == 1 && (src.in_fs * 4) % 16 == 0) {
-        x.fmt = 2;
-    }
+    if ((inA & 7) == 0 && C == 2 && src.in_fs == 2 && src.in_cs == 1) x.fmt = 1;
+    else if ((inA & 15) == 0 && C % 4 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) x.fmt = 2;
     static const bool noFmt = std::getenv("GAR_HX_DWORD") != nullptr;
     if (noFmt) x.fmt = 0;
     x.src = src;
@@ -156,29 +155,22 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
 
     const size_t lds = ldsFor(G, parity);
     const int64_t blocks = std::min<int64_t>(x.nblocks, ncu);
+    x.nprog = p.nw;
     if (p.rb) {
         if (p.nw > kHxRbMaxWaves) return hipErrorInvalidConfiguration;
-        const int waves = p.nw;
+        const int waves = std::max(p.nw, kHxMinWaves);
         switch (p.NS) {
-            case 1: return hxDispatch<1, true>(x, waves, lds, blocks, stream);
-            case 2: return hxDispatch<2, true>(x, waves, lds, blocks, stream);
-            case 3: return hxDispatch<3, true>(x, waves, lds, blocks, stream);
-            case 4: return hxDispatch<4, true>(x, waves, lds, blocks, stream);
-            case 5: return hxDispatch<5, true>(x, waves, lds, blocks, stream);
-            case 6: return hxDispatch<6, true>(x, waves, lds, blocks, stream);
-            case 7: return hxDispatch<7, true>(x, waves, lds, blocks, stream);
-            case 8: return hxDispatch<8, true>(x, waves, lds, blocks, stream);
-            case 9: return hxDispatch<9, true>(x, waves, lds, blocks, stream);
-            case 10: return hxDispatch<10, true>(x, waves, lds, blocks, stream);
+#define GAR_HX_RB(n) case n: return hxDispatch<n, true>(x, waves, lds, blocks, stream);
+            GAR_HX_RB(1) GAR_HX_RB(2) GAR_HX_RB(3) GAR_HX_RB(4) GAR_HX_RB(5) GAR_HX_RB(6) GAR_HX_RB(7) GAR_HX_RB(8)
+            GAR_HX_RB(9) GAR_HX_RB(10)
+#undef GAR_HX_RB
             default: return hipErrorInvalidConfiguration;
         }
     }
     switch (p.NS) {
-        case 2: return hxDispatch<2, false>(x, kHxWaves, lds, blocks, stream);
-        case 4: return hxDispatch<4, false>(x, kHxWaves, lds, blocks, stream);
-        case 6: return hxDispatch<6, false>(x, kHxWaves, lds, blocks, stream);
-        case 8: return hxDispatch<8, false>(x, kHxWaves, lds, blocks, stream);
-        case 10: return hxDispatch<10, false>(x, kHxWaves, lds, blocks, stream);
+#define GAR_HX_SEG(n) case n: return hxDispatch<n, false>(x, kHxWaves, lds, blocks, stream);
+        GAR_HX_SEG(2) GAR_HX_SEG(4) GAR_HX_SEG(6) GAR_HX_SEG(8)
+#undef GAR_HX_SEG
         default: return hipErrorInvalidConfiguration;
     }
 }

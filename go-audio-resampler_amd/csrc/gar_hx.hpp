@@ -10,13 +10,15 @@
 // and the f16 MFMA retires 16x the MACs per cycle of the f32 one.
 //
 // One block = 16 columns (channel x chunk of G macro periods) staged in LDS
-// as f16 hi/lo images (double-buffered).  Workgroup = nwc compute waves + 2
-// stager waves: while the compute waves run block b from one buffer, the
-// stagers LDS-DMA block b+grid's raw f32 windows into the other buffer and
-// convert them in place.  Row-block mode (RB): compute wave w owns row block
-// w over its whole band (A in registers, no partial sums: one barrier per
-// block).  Segmented mode: 8 balanced wave programs of up to 3 row-block
-// segments with LDS partial-sum reduction (as bg_kernel).
+// as f16 hi/lo images (double-buffered).  Every wave of the workgroup both
+// computes and stages: at the top of block b it issues the global loads of
+// block b+grid's raw f32 windows into registers (a few items per lane), runs
+// its MFMA program over block b (the loads land meanwhile), then publishes
+// its per-quad max |x| (LDS atomic max), and after one barrier converts its
+// items into the other image buffer.  Row-block mode (RB): wave w owns row
+// block w over its whole band (A in registers, no partial sums).  Segmented
+// mode: 8 balanced wave programs of up to 3 row-block segments with LDS
+// partial-sum reduction (as bg_kernel).
 // Blocks holding Inf/NaN are skipped and recomputed with a plain f32 FIR over
 // the exact rows by the last workgroup to finish (IEEE propagation).
 #pragma once
@@ -27,10 +29,12 @@ namespace gar {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef short s8v __attribute__((ext_vector_type(8)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s4v* lds_s4p;
 
 constexpr int kHxNonFinite = 0x40000000;
-constexpr int kHxRpl = kHxMaxRows / 64;  // window rows per stager lane
+constexpr int kHxJ = (4 * kHxMaxRows + 64 * kHxMinWaves - 1) / (64 * kHxMinWaves);  // staged row items per lane
 
 __device__ __forceinline__ s4v trRead(const char* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4p)p); }
 
@@ -51,8 +55,8 @@ struct HxArgs {
     int* fix;              // non-finite block list (HxDev::fix)
     int fixCap, ea, kch;
     int Pc, Qc, W, Ws, G, C, ncols, nblocks, nred, nslots, parity, vst, dbg;
-    int fmt;               // raw staging format: 0 dword gather, 1 stereo frame pairs (x4), 2 four channels (x4)
-    int par0, gqOdd;       // fmt 1: parity of chunk 0's first frame in the input, parity of G*Qc
+    int fmt;               // raw load format: 0 dword gather, 1 stereo frames (x2 loads), 2 four channels (x4 loads)
+    int nprog;             // wave programs (waves >= nprog only stage)
     const float* in;       // element (row 0 of chunk 0's window, channel 0)
     int64_t in_fs, in_cs, in_chunk;          // elements per row, per channel, per chunk
     char* out;             // byte address of output (row 0 of chunk 0, channel 0)
@@ -69,201 +73,156 @@ struct HxArgs {
     const float* zero;
 };
 
-// Staging parameters, by value into the (out-of-line) stager routine.
-struct HxStage {
-    const float* in;
-    const float* zero;
-    int64_t in_fs, in_cs, in_chunk;
-    int W, Ws, C, ncols, fmt, par0, gqOdd;
-};
-
-typedef const __attribute__((address_space(4))) HxArgs* HxKarg;  // the kernel's argument block
-
-template <class X>
-__device__ __forceinline__ HxStage hxStageArgs(const X& x) {
-    HxStage t;
-    t.in = x.in; t.zero = x.zero;
-    t.in_fs = x.in_fs; t.in_cs = x.in_cs; t.in_chunk = x.in_chunk;
-    t.W = x.W; t.Ws = x.Ws; t.C = x.C; t.ncols = x.ncols; t.fmt = x.fmt; t.par0 = x.par0; t.gqOdd = x.gqOdd;
-    return t;
-}
-
 // ---- staging ----------------------------------------------------------------
-// Two stager waves per workgroup stage the NEXT block while the compute waves
-// run the current one; stager s owns column quads 2s and 2s+1.  Image buffer
-// layout, quad-major: quad q (columns 4q..4q+3) occupies bytes
-// [q*QS, q*QS + 16*Ws), QS = 16*Ws + 64: hi rows (4 f16 = 8 B each) then lo
-// rows.  The quad's raw f32 window is LDS-DMA'd (global_load_lds_dword, no
-// registers) into the same bytes ([4 columns][Ws] f32), then converted in
-// place by the one wave that owns it -- no cross-wave synchronisation.  The
-// +64 B skew puts the four quads of any 8 consecutive rows on distinct banks
-// for ds_read_b64_tr_b16.  Rows >= W are clamped to row W-1 (finite; A is
-// zero there); columns past the launch read zeros.
+// Image buffer layout: quad q (columns 4q..4q+3) at q*QS, QS = 16*Ws + 64: hi
+// rows (4 f16 = 8 B each) then lo rows; the +64 B skew puts the four quads of
+// any 8 consecutive rows on distinct banks for ds_read_b64_tr_b16.
+// Items: the block's 4*Ws (quad, row) pairs; item t = (wave + NW*j)*64 + lane
+// for j < kHxJ, so each wave-instruction's 64 items are 64 consecutive rows of
+// one quad (Ws % 64 == 0) and its loads coalesce.  Rows >= W are clamped to
+// row W-1 (finite; A is zero there); columns past the launch read zeros.
 __device__ __forceinline__ uint32_t hxQS(int Ws) { return 16u * static_cast<uint32_t>(Ws) + 64u; }
 
-// (uniform operands made provably scalar: readfirstlane of the LDS address and base)
-__device__ __forceinline__ const char* uniPtr(const char* p) {
-    const uint64_t v = reinterpret_cast<uint64_t>(p);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
-    return reinterpret_cast<const char*>((static_cast<uint64_t>(hi) << 32) | lo);
+struct HxItems {
+    int q[kHxJ];     // quad of item slot j (wave-uniform), -1: none
+    int r0[kHxJ];    // first row of the slot's 64 rows
+};
+
+__device__ __forceinline__ HxItems hxItems(int Ws, int wt, int NW) {
+    HxItems it;
+#pragma unroll
+    for (int j = 0; j < kHxJ; ++j) {
+        const int tb = (wt + NW * j) * 64;
+        const int q = tb < 4 * Ws ? tb / Ws : -1;
+        it.q[j] = uni(q);
+        it.r0[j] = uni(q >= 0 ? tb - q * Ws : 0);
+    }
+    return it;
 }
 
-__device__ __forceinline__ void hxDmaOne(uint32_t lds, uint32_t voff, const char* base) {
-    lds = __builtin_amdgcn_readfirstlane(lds);
-    base = uniPtr(base);
-    // inline asm: the compiler would otherwise treat every later LDS read as aliasing
-    // this DMA and drain vmcnt before it (the stager waits for it explicitly)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2" :: "s"(lds), "v"(voff), "s"(base) : "m0");
-}
-__device__ __forceinline__ void hxDmaOne4(uint32_t lds, uint32_t voff, const char* base) {
-    lds = __builtin_amdgcn_readfirstlane(lds);
-    base = uniPtr(base);
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" :: "s"(lds), "v"(voff), "s"(base) : "m0");
+// Raw buffer loads: a wave-uniform resource (SGPRs) per chunk/column base and a
+// 32-bit lane offset; the compiler tracks them as loads (vmcnt) and keeps the
+// 64-bit address math scalar.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxRsrc(const float* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
 }
 
-// Stereo (fmt 1): a column quad = 2 chunks x 2 channels; chunk jj's window is
-// fetched as 16-B frame pairs starting at an even input frame (off = 1 when
-// the window starts at an odd one: one leading row), raw [jj][row + off][2].
-__device__ __forceinline__ int hxStereoOff(const HxStage& x, int ck) { return (x.par0 + ck * x.gqOdd) & 1; }
-
-__device__ __forceinline__ void hxDmaQuad(const HxStage& x, int b, int q, int lane, char* buf) {
-    const uint32_t qbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(buf + q * hxQS(x.Ws))));
-    const int wl = x.W - 1;
-    if (x.fmt == 1) {
+// Global loads of block bl's items into registers (issued, not waited on).
+// Every slot loads unconditionally (columns past the launch read column 0's
+// chunk and are zeroed afterwards), so no branch separates a load from its use.
+__device__ __forceinline__ void hxLoad(const HxArgs& x, const HxItems& it, int bl, int lane, f32x4 (&v)[kHxJ]) {
+    const uint32_t fsB = static_cast<uint32_t>(x.in_fs) * 4u;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int col = b * 16 + 4 * q + 2 * jj;
-            const bool ok = col < x.ncols;
-            const int ck = col >> 1;
-            const int off = hxStereoOff(x, ck);
-            const char* base = ok ? reinterpret_cast<const char*>(x.in + ck * x.in_chunk - 2 * off)
-                                  : reinterpret_cast<const char*>(x.zero);
-            const int mmax = (wl + off) >> 1;
-            const uint32_t l0 = qbase + 8u * static_cast<uint32_t>(x.Ws) * jj;
-#pragma unroll
-            for (int k = 0; k < kHxRpl / 2; ++k) {
-                if (128 * k >= x.Ws) break;
-                const uint32_t voff = ok ? static_cast<uint32_t>(min(64 * k + lane, mmax)) * 16u : 0u;
-                hxDmaOne4(l0 + 1024u * k, voff, base);
-            }
-        }
-        return;
-    }
-    if (x.fmt == 2) {
-        const int col = b * 16 + 4 * q;
-        const bool ok = col < x.ncols;
-        const int ck = col / x.C, c0 = col - ck * x.C;
-        const char* base = ok ? reinterpret_cast<const char*>(x.in + ck * x.in_chunk + c0)
-                              : reinterpret_cast<const char*>(x.zero);
-        const uint32_t sb = ok ? static_cast<uint32_t>(x.in_fs) * 4u : 0u;
-#pragma unroll
-        for (int k = 0; k < kHxRpl; ++k) {
-            if (64 * k >= x.Ws) break;
-            hxDmaOne4(qbase + 1024u * k, static_cast<uint32_t>(min(64 * k + lane, wl)) * sb, base);
-        }
-        return;
-    }
-    const uint32_t sb = static_cast<uint32_t>(x.in_fs) * 4u;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const int col = b * 16 + 4 * q + n;
-        const bool ok = col < x.ncols;
-        const int ck = col / x.C, c = col - ck * x.C;
-        const char* base = ok ? reinterpret_cast<const char*>(x.in + ck * x.in_chunk + c * x.in_cs)
-                              : reinterpret_cast<const char*>(x.zero);
-        const uint32_t sbn = ok ? sb : 0u;
-        const uint32_t l0 = qbase + 4u * static_cast<uint32_t>(x.Ws) * n;
-#pragma unroll
-        for (int k = 0; k < kHxRpl; ++k) {
-            if (k >= (x.Ws >> 6)) break;
-            hxDmaOne(l0 + 256u * k, static_cast<uint32_t>(min(64 * k + lane, wl)) * sbn, base);
-        }
-    }
-}
-
-// max |x| bits of a lane's values -> wave max -> scale exponent (max * 2^e in
-// [2^14, 2^15)) or the non-finite flag, published in ce[4q..4q+3].
-__device__ __forceinline__ int hxQuadExp(uint32_t mu, int q, int lane, int* ce) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mu = max(mu, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mu), o)));
-    mu = static_cast<uint32_t>(uni(static_cast<int>(mu)));
-    int e = 0;
-    if (mu >= 0x7f800000u) {
-        e = kHxNonFinite;
-    } else if (mu != 0) {
-        int ex;
-        (void)frexpf(__uint_as_float(mu), &ex);
-        e = 15 - ex;
-    }
-    e = uni(e);
-    if (lane < 4) ce[4 * q + lane] = e;
-    return e;
-}
-
-__device__ __forceinline__ void hxPutRow(char* qb, int Ws, int r, int e, const float (&v)[4]) {
-    s4v hv, lv;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-        const float xs = ldexpf(v[n], e);
-        const _Float16 hh = static_cast<_Float16>(xs);
-        const _Float16 ll = static_cast<_Float16>(xs - static_cast<float>(hh));
-        hv[n] = __builtin_bit_cast(short, hh);
-        lv[n] = __builtin_bit_cast(short, ll);
-    }
-    *reinterpret_cast<s4v*>(qb + 8 * r) = hv;
-    *reinterpret_cast<s4v*>(qb + 8 * Ws + 8 * r) = lv;
-}
-
-// Raw quad (layout FMT, see hxDmaQuad) -> registers; scale exponent; f16 hi/lo
-// rows written over the raw (every raw value is in registers before the first
-// write).  Rows >= Ws (register slots past the window) are not touched.
-template <int FMT>
-__device__ __forceinline__ void hxConvertQuadF(const HxStage& x, int b, int q, int lane, char* buf, int* ce) {
-    char* qb = buf + q * hxQS(x.Ws);
-    const float* rf = reinterpret_cast<const float*>(qb);
-    const int nr = x.Ws >> 6;
-    int o0 = 0, o1 = 0;
-    if (FMT == 1) {
-        const int ck0 = (b * 16 + 4 * q) >> 1;
-        o0 = hxStereoOff(x, ck0);
-        o1 = hxStereoOff(x, ck0 + 1);
-    }
-    float v[kHxRpl][4];
-    uint32_t mu = 0;
-#pragma unroll
-    for (int i = 0; i < kHxRpl; ++i) {
-        const int r = min(64 * i, 64 * (nr - 1)) + lane;  // slots past the window repeat the last chunk
-        if (FMT == 1) {
-            const float2 a = *reinterpret_cast<const float2*>(rf + 2 * (r + o0));
-            const float2 c = *reinterpret_cast<const float2*>(rf + 2 * x.Ws + 2 * (r + o1));
-            v[i][0] = a.x; v[i][1] = a.y; v[i][2] = c.x; v[i][3] = c.y;
-        } else if (FMT == 2) {
-            const f32x4 a = *reinterpret_cast<const f32x4*>(rf + 4 * r);
-            v[i][0] = a[0]; v[i][1] = a[1]; v[i][2] = a[2]; v[i][3] = a[3];
+    for (int j = 0; j < kHxJ; ++j) {
+        if (it.q[j] < 0) continue;
+        const int off = static_cast<int>(static_cast<uint32_t>(min(it.r0[j] + lane, x.W - 1)) * fsB);
+        const int col = bl * 16 + 4 * it.q[j];
+        if (x.fmt == 1) {  // stereo frames: chunks col/2 and col/2 + 1, both channels
+            const int ck0 = col < x.ncols ? col >> 1 : 0, ck1 = col + 2 < x.ncols ? (col >> 1) + 1 : 0;
+            const f2v a = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      hxRsrc(x.in + static_cast<int64_t>(ck0) * x.in_chunk), off, 0, 0));
+            const f2v c = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      hxRsrc(x.in + static_cast<int64_t>(ck1) * x.in_chunk), off, 0, 0));
+            v[j] = f32x4{a.x, a.y, c.x, c.y};
+        } else if (x.fmt == 2) {  // four contiguous channels of one chunk
+            const int cc = col < x.ncols ? col : 0;
+            const int ck = cc / x.C, c0 = cc - ck * x.C;
+            v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hxRsrc(x.in + ck * x.in_chunk + c0), off, 0, 0));
         } else {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) v[i][n] = rf[n * x.Ws + r];
+            for (int n = 0; n < 4; ++n) {
+                const int cn = col + n < x.ncols ? col + n : 0;
+                const int ck = cn / x.C, c = cn - ck * x.C;
+                v[j][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                         hxRsrc(x.in + ck * x.in_chunk + c * x.in_cs), off, 0, 0));
+            }
         }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) mu = max(mu, __float_as_uint(v[i][n]) & 0x7fffffffu);
     }
-    const int e = hxQuadExp(mu, q, lane, ce);
-    if (e == kHxNonFinite) return;
-#pragma unroll
-    for (int i = 0; i < kHxRpl; ++i)
-        if (i < nr) hxPutRow(qb, x.Ws, 64 * i + lane, e, v[i]);
 }
 
-// Stager s: block b's quads 2s, 2s+1 into image buffer buf (DMA, wait, convert).
-template <int FMT>
-__device__ __noinline__ void hxStageF(HxKarg xp, int b, int s, int lane, char* buf, int* ce) {
-    const HxStage x = hxStageArgs(*xp);  // uniform fields: scalar loads from the kernarg segment
-    hxDmaQuad(x, b, 2 * s, lane, buf);
-    hxDmaQuad(x, b, 2 * s + 1, lane, buf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA landed
-    hxConvertQuadF<FMT>(x, b, 2 * s, lane, buf, ce);
-    hxConvertQuadF<FMT>(x, b, 2 * s + 1, lane, buf, ce);
+// Zero the lanes of item slots whose columns lie past the launch (after the loads landed).
+__device__ __forceinline__ void hxMaskCols(const HxArgs& x, const HxItems& it, int bl, f32x4 (&v)[kHxJ]) {
+#pragma unroll
+    for (int j = 0; j < kHxJ; ++j) {
+        if (it.q[j] < 0) continue;
+        const int col = bl * 16 + 4 * it.q[j];
+        if (col + 4 <= x.ncols) continue;  // uniform: whole quad inside
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            if (col + n >= x.ncols) v[j][n] = 0.f;
+    }
+}
+
+// Wave max of non-negative u32 (DPP row shifts + row broadcasts; lane 63).
+__device__ __forceinline__ uint32_t hxWaveMax(uint32_t v) {
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, true)));
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, true)));
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, true)));
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, true)));
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
+    v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 63));
+}
+
+// Per-quad max |x| bits (Inf/NaN -> 0x7f800000 via an x*0 accumulator) into
+// the LDS slots qe[0..3] (atomic max; one lane per item slot).
+__device__ __forceinline__ void hxPublishMax(const HxItems& it, f32x4 (&v)[kHxJ], int lane, uint32_t* qe) {
+    const f2v z = {0.f, 0.f};
+    // every item slot's load settled here, and the registers re-defined as
+    // plain values: else the compiler waits vmcnt(0) again where the items are
+    // converted -- by then for the MFMA epilogue's stores
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int j = 0; j < kHxJ; ++j) asm volatile("" : "+v"(v[j]));
+#pragma unroll
+    for (int j = 0; j < kHxJ; ++j) {
+        if (it.q[j] < 0) continue;
+        const f2v v01 = {v[j][0], v[j][1]}, v23 = {v[j][2], v[j][3]};
+        const f2v nacc = __builtin_elementwise_fma(v23, z, __builtin_elementwise_fma(v01, z, z));
+        const float m = fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])), fmaxf(fabsf(v[j][2]), fabsf(v[j][3])));
+        uint32_t mu = __float_as_uint(m);
+        if (!(nacc.x == 0.f && nacc.y == 0.f)) mu = 0x7f800000u;
+        mu = hxWaveMax(mu);
+        if (lane == 0) atomicMax(qe + it.q[j], mu);
+    }
+}
+
+// Scale exponent of a quad from its max bits: max * 2^e in [2^14, 2^15);
+// kHxNonFinite (block goes to the exact slow path) for Inf/NaN, or when the
+// quad is so small (max < 2^-111, denormals included) that 2^e is no f32.
+__device__ __forceinline__ int hxExpOf(uint32_t mu) {
+    if (mu >= 0x7f800000u) return kHxNonFinite;
+    if (mu == 0) return 0;
+    const int E = static_cast<int>(mu >> 23);
+    return E < 15 ? kHxNonFinite : 141 - E;
+}
+
+// One window row (4 columns) -> f16 hi and lo rows: xs = x * 2^e (exact),
+// hi = f16(xs), lo = f16(xs - hi); packed f32 / f16 pair conversions.
+__device__ __forceinline__ void hxPutRow(char* qb, int Ws, int r, f2v sc, f2v v01, f2v v23) {
+    const f2v a = v01 * sc, c = v23 * sc;
+    const h2v ah = __builtin_convertvector(a, h2v), ch = __builtin_convertvector(c, h2v);
+    const h2v al = __builtin_convertvector(a - __builtin_convertvector(ah, f2v), h2v);
+    const h2v cl = __builtin_convertvector(c - __builtin_convertvector(ch, f2v), h2v);
+    uint2 hv, lv;
+    hv.x = __builtin_bit_cast(uint32_t, ah); hv.y = __builtin_bit_cast(uint32_t, ch);
+    lv.x = __builtin_bit_cast(uint32_t, al); lv.y = __builtin_bit_cast(uint32_t, cl);
+    *reinterpret_cast<uint2*>(qb + 8 * r) = hv;
+    *reinterpret_cast<uint2*>(qb + 8 * Ws + 8 * r) = lv;
+}
+
+// Items -> f16 hi/lo rows of image buffer buf (quad exponents from qe).
+__device__ __forceinline__ void hxConvert(const HxItems& it, const f32x4 (&v)[kHxJ], int Ws, int lane, char* buf,
+                                          const uint32_t* qe) {
+    const uint32_t QS = hxQS(Ws);
+#pragma unroll
+    for (int j = 0; j < kHxJ; ++j) {
+        if (it.q[j] < 0) continue;
+        const int e = hxExpOf(qe[it.q[j]]);
+        if (e == kHxNonFinite) continue;  // block is recomputed by the slow path
+        const float s1 = __uint_as_float(static_cast<uint32_t>(e + 127) << 23);
+        hxPutRow(buf + it.q[j] * QS, Ws, it.r0[j] + lane, f2v{s1, s1}, f2v{v[j][0], v[j][1]}, f2v{v[j][2], v[j][3]});
+    }
 }
 
 // B fragment (32 K x 16 columns) at the lane's transposed-read address p:
@@ -372,127 +331,144 @@ __device__ __forceinline__ void hxFixup(const HxArgs& x, int* s_last) {
     }
 }
 
-// Compute waves: RB (row-block mode) <= kHxRbMaxWaves, else kHxWaves
-// segmented programs; + 2 stager waves.
-template <bool RB>
-constexpr int hxThreads() { return 64 * ((RB ? kHxRbMaxWaves : kHxWaves) + 2); }
-
 template <int NS, bool RB, bool SINGLE>
-__global__ __launch_bounds__(hxThreads<RB>()) void hx_kernel(HxArgs x, int nwc) {
+__global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t QS = hxQS(x.Ws);
     const uint32_t bufB = 4 * QS;
     char* imgs = reinterpret_cast<char*>(smem);  // [2][4 quads][QS]
     float* part = reinterpret_cast<float*>(smem + 2 * static_cast<size_t>(bufB));
     const int partStride = x.nslots * 256;
-    int* colExp = reinterpret_cast<int*>(part + (x.parity ? 2 : 1) * partStride);  // [2][16] + fixup flag
+    uint32_t* qeAll = reinterpret_cast<uint32_t*>(part + (x.parity ? 2 : 1) * partStride);  // [4 sets][4 quads] + fixup flag
 
+    const int NW = blockDim.x >> 6;
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
     const int nbar = RB ? 0 : (x.nred > 0 ? (x.parity ? 1 : 2) : 0);  // barriers per macro period
+    const bool hasProg = wt < x.nprog;
 
-    if (wt >= nwc) {
-        // ---- stager wave: quads 2s, 2s+1 of every next block (it = -1: prologue, buffer 0) ----
-        const int s = wt - nwc;
-        int b = blockIdx.x;
-        for (int it = -1; b < x.nblocks && !(x.dbg & 16); ++it) {
-            if (it >= 0) __syncthreads();  // buffer it&1 staged; buffer (it+1)&1 free
-            const int bs = it < 0 ? b : b + gridDim.x;
-            const int ib = it < 0 ? 0 : ((it & 1) ^ 1);
-            if (bs < x.nblocks && !(it >= 0 && (x.dbg & 1))) {
-                char* buf = imgs + static_cast<size_t>(ib) * bufB;
-                int* ce = colExp + ib * 16;
-                const HxKarg st = (HxKarg)__builtin_amdgcn_kernarg_segment_ptr();
-                if (x.fmt == 1) hxStageF<1>(st, bs, s, lane, buf, ce);
-                else if (x.fmt == 2) hxStageF<2>(st, bs, s, lane, buf, ce);
-                else hxStageF<0>(st, bs, s, lane, buf, ce);
-            }
-            if (it >= 0) {
-                for (int gi = 0; gi < x.G; ++gi)
-                    for (int k = 0; k < nbar; ++k) __syncthreads();
-                b += gridDim.x;
-            }
-        }
-    } else {
-        // ---- compute wave ----
-        const int grp = lane >> 4, l16 = lane & 15;
-        // transposed-read address of this lane: quad (l16 & 3), row 4*grp + (l16 >> 2)
-        const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
-        const ProgU pu = progLoad(x.progs + kBgProgInts * wt);  // one program per wave
-        const int u0 = pu.u0, rbw = pu.rb0;
-        h8v Ah[NS], Al[NS];
-        if (SINGLE) {
+    const int grp = lane >> 4, l16 = lane & 15;
+    // transposed-read address of this lane: quad (l16 & 3), row 4*grp + (l16 >> 2)
+    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+    const ProgU pu = progLoad(x.progs + kBgProgInts * (hasProg ? wt : 0));
+    const int nseg = hasProg ? pu.nseg : 0;
+    const int plen = uni(x.progs[kBgProgInts * (hasProg ? wt : 0) + 15]);  // program steps (rest: zero A)
+    auto uPad = [&](int st) { return st < plen ? selU(pu, st) : -kHxStep * plen; };
+    const int u0 = pu.u0, rbw = pu.rb0;
+    h8v Ah[NS], Al[NS];
+    if (SINGLE) {
 #pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
-                Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): A settled before the loop
+        for (int s = 0; s < NS; ++s) {
+            Ah[s] = x.A[((static_cast<size_t>(hasProg ? wt : 0) * NS + s) * 2 + 0) * 64 + lane];
+            Al[s] = x.A[((static_cast<size_t>(hasProg ? wt : 0) * NS + s) * 2 + 1) * 64 + lane];
         }
-        int q = 0;
-        for (int b = blockIdx.x, it = 0; b < x.nblocks && !(x.dbg & 16); b += gridDim.x, ++it) {
-            __syncthreads();  // buffer it&1 staged; buffer (it+1)&1 free
-            const int cur = it & 1;
-            const char* imgH = imgs + static_cast<size_t>(cur) * bufB + laneOff;
-            const char* imgL = imgH + 8 * x.Ws;
-            const int myE = colExp[cur * 16 + l16];
-            const bool nonFinite = __any(myE == kHxNonFinite);
-            const int sh = -(x.ea + myE);
-            const int col = b * 16 + l16;
-            const bool colOk = col < x.ncols;
-            const int chunk = col / x.C, c = col - chunk * x.C;
+        // vmcnt(0): A settled on every path into the block loop (else the compiler
+        // flushes vmcnt before the MFMA loop -- and with it the staging loads)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
 
-            if (nonFinite) {
-                if (wt == 0 && lane == 0) {
-                    const int k = atomicAdd(&x.fix[0], 1);
-                    if (k < x.fixCap) x.fix[2 + k] = b;
-                }
-                for (int gi = 0; gi < x.G; ++gi, ++q)
-                    for (int k = 0; k < nbar; ++k) __syncthreads();
-                continue;
+    // Staging pipeline (one barrier per block): iteration it computes block
+    // b_it from buffer it&1 while, in the same barrier interval, converting
+    // b_{it+1} (loaded + max-published during iteration it-1) into the other
+    // buffer, then loading b_{it+2} into registers (landing during the MFMA
+    // work) and publishing its quad maxima at the end.  Exponent sets rotate
+    // over 4 (block k uses set k & 3): iteration it reads sets it, it+1, writes
+    // it+2 and zeroes it+3 (last read in iteration it-1).
+    const HxItems items = hxItems(x.Ws, wt, NW);
+    f32x4 raw[kHxJ];
+    if (threadIdx.x < 16) qeAll[threadIdx.x] = 0;
+    int b = blockIdx.x;
+    const int G2 = static_cast<int>(gridDim.x);
+    const bool staging = !(x.dbg & 1);
+    if (b < x.nblocks && !(x.dbg & 16)) {  // prologue: block b -> buffer 0 (set 0), block b+grid -> registers (set 1)
+        hxLoad(x, items, b, lane, raw);
+        __syncthreads();  // sets zeroed
+        hxMaskCols(x, items, b, raw);
+        hxPublishMax(items, raw, lane, qeAll);
+        __syncthreads();
+        hxConvert(items, raw, x.Ws, lane, imgs, qeAll);
+        if (b + G2 < x.nblocks) {
+            hxLoad(x, items, b + G2, lane, raw);
+            hxMaskCols(x, items, b + G2, raw);
+            hxPublishMax(items, raw, lane, qeAll + 4);
+        }
+    }
+    int q = 0;
+    for (int it = 0; b < x.nblocks && !(x.dbg & 16); b += G2, ++it) {
+        __syncthreads();  // buffer it&1 staged, set it+1 published; buffer (it+1)&1 free
+        const uint32_t* qeCur = qeAll + 4 * (it & 3);
+        if (threadIdx.x < 4) qeAll[4 * ((it + 3) & 3) + threadIdx.x] = 0;
+        const int b1 = b + G2, b2 = b1 + G2;
+        if (b1 < x.nblocks && staging)
+            hxConvert(items, raw, x.Ws, lane, imgs + static_cast<size_t>((it + 1) & 1) * bufB, qeAll + 4 * ((it + 1) & 3));
+        const bool more = b2 < x.nblocks && staging;
+        if (more) hxLoad(x, items, b2, lane, raw);
+
+        const int cur = it & 1;
+        const char* imgH = imgs + static_cast<size_t>(cur) * bufB + laneOff;
+        const char* imgL = imgH + 8 * x.Ws;
+        const int myE = hxExpOf(qeCur[l16 >> 2]);
+        const bool nonFinite = __any(myE == kHxNonFinite);
+        const int sh = -(x.ea + myE);
+        const int col = b * 16 + l16;
+        const bool colOk = col < x.ncols;
+        const int chunk = col / x.C, c = col - chunk * x.C;
+
+        if (nonFinite) {
+            if (wt == 0 && lane == 0) {
+                const int k = atomicAdd(&x.fix[0], 1);
+                if (k < x.fixCap) x.fix[2 + k] = b;
             }
-            if (RB) {
-                if (pu.nseg > 0 && !(x.dbg & 2)) {
-                    char* optr = hxOutPtr(x, chunk, c, 0, rbw * 16 + 4 * grp, lane);
-                    const int64_t ostep = static_cast<int64_t>(x.Pc) * x.out_fs;
-                    const bool full = (rbw + 1) * 16 <= x.Pc;
-                    for (int gi = 0; gi < x.G; ++gi) {
-                        // step s reads rows 32 s further: +256 B
-                        const uint32_t ro = 8u * static_cast<uint32_t>(gi * x.Qc + u0);
-                        const char* ph = imgH + ro;
-                        const char* pl = imgL + ro;
-                        f32x4 accB = {0, 0, 0, 0}, accS = accB;
-                        h8v bh0 = bFragQ(ph), bl0 = bFragQ(pl), bh1, bl1;
-                        if (NS > 1) { bh1 = bFragQ(ph + 256); bl1 = bFragQ(pl + 256); }
+            for (int gi = 0; gi < x.G; ++gi, ++q)
+                for (int k = 0; k < nbar; ++k) __syncthreads();
+        } else if (RB) {
+            if (nseg > 0 && !(x.dbg & 2)) {
+                const bool full = (rbw + 1) * 16 <= x.Pc;
+                // full row blocks: hxPut4 layout; partial: rows r0 + i of the lane's column
+                char* optr = full ? hxOutPtr(x, chunk, c, 0, rbw * 16 + 4 * grp, lane)
+                                  : x.out + chunk * x.out_chunk + c * x.out_cs + (rbw * 16 + 4 * grp) * x.out_fs;
+                const int64_t ostep = static_cast<int64_t>(x.Pc) * x.out_fs;
+                // the wave's step stream: element u = step u % NS of period u / NS at
+                // rows gi*Qc + u0 + 32 s (+8 B per row); B runs one element ahead,
+                // across periods (reads past the last period land inside LDS, unused)
+                const uint32_t gstep = 8u * static_cast<uint32_t>(x.Qc);
+                const char* ph = imgH + 8u * static_cast<uint32_t>(u0);
+                const char* pl = imgL + 8u * static_cast<uint32_t>(u0);
+                h8v bh0 = bFragQ(ph), bl0 = bFragQ(pl);
+                for (int gi = 0; gi < x.G; ++gi) {
+                    f32x4 accB = {0, 0, 0, 0}, accS = accB;
 #pragma unroll
-                        for (int s = 0; s < NS; ++s) {
-                            h8v bh2, bl2;
-                            if (s + 2 < NS) {
-                                bh2 = bFragQ(ph + 256 * (s + 2));
-                                bl2 = bFragQ(pl + 256 * (s + 2));
-                            }
-                            accB = mfma16(Ah[s], bh0, accB);
-                            accS = mfma16(Ah[s], bl0, accS);
-                            accS = mfma16(Al[s], bh0, accS);
-                            bh0 = bh1; bl0 = bl1;
-                            if (s + 2 < NS) { bh1 = bh2; bl1 = bl2; }
-                        }
-                        const f32x4 y = hxScale(accB + accS, sh);
-                        if (full) {
-                            if (colOk) hxPut4(x, optr, y, lane);
-                        } else {  // partial last row block: rows < Pc only
-#pragma unroll
-                            for (int i = 0; i < 4; ++i)
-                                if (colOk && rbw * 16 + 4 * grp + i < x.Pc) hxPut1(x, chunk, c, gi, rbw * 16 + 4 * grp + i, y[i]);
-                        }
-                        optr += ostep;
+                    for (int s = 0; s < NS; ++s) {
+                        const char* nh = s + 1 < NS ? ph + 256 * (s + 1) : ph + gstep;
+                        const char* nl = s + 1 < NS ? pl + 256 * (s + 1) : pl + gstep;
+                        const h8v bh1 = bFragQ(nh), bl1 = bFragQ(nl);
+                        accB = mfma16(Ah[s], bh0, accB);
+                        accS = mfma16(Ah[s], bl0, accS);
+                        accS = mfma16(Al[s], bh0, accS);
+                        bh0 = bh1; bl0 = bl1;
+                        __builtin_amdgcn_sched_barrier(0);  // keep reads(s + 1) -> MFMAs(s) order per step
                     }
+                    ph += gstep;
+                    pl += gstep;
+                    const f32x4 y = hxScale(accB + accS, sh);
+                    if (full) {
+                        if (colOk) hxPut4(x, optr, y, lane);
+                    } else {  // partial last row block: rows < Pc only
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (colOk && rbw * 16 + 4 * grp + i < x.Pc) {
+                                char* pp = optr + i * x.out_fs;
+                                if (x.out_f64) *reinterpret_cast<double*>(pp) = y[i];
+                                else *reinterpret_cast<float*>(pp) = y[i];
+                            }
+                    }
+                    optr += ostep;
                 }
-                continue;
             }
+        } else {
             for (int gi = 0; gi < x.G; ++gi, ++q) {
                 float* pslots = part + static_cast<size_t>(x.parity ? (q & 1) : 0) * partStride;
-                if (pu.nseg > 0 && !(x.dbg & 2)) {
+                if (nseg > 0 && !(x.dbg & 2)) {
                     f32x4 accB = {0, 0, 0, 0}, accS = accB, r0 = accB, r1 = accB;
                     for (int ch = 0; ch < (SINGLE ? 1 : x.kch); ++ch) {
                         const int sb = SINGLE ? 0 : ch * NS;
@@ -504,14 +480,14 @@ __global__ __launch_bounds__(hxThreads<RB>()) void hx_kernel(HxArgs x, int nwc) 
                             }
                         }
                         const int rowg = gi * x.Qc;
-                        const uint32_t ad = 8u * static_cast<uint32_t>(rowg + selU(pu, sb) + kHxStep * sb);
+                        const uint32_t ad = 8u * static_cast<uint32_t>(rowg + uPad(sb) + kHxStep * sb);
                         h8v bh = bFragQ(imgH + ad), bl = bFragQ(imgL + ad);
 #pragma unroll
                         for (int s = 0; s < NS; ++s) {
                             h8v nh, nl;
                             if (s + 1 < NS) {
                                 const uint32_t an =
-                                    8u * static_cast<uint32_t>(rowg + selU(pu, sb + s + 1) + kHxStep * (sb + s + 1));
+                                    8u * static_cast<uint32_t>(rowg + uPad(sb + s + 1) + kHxStep * (sb + s + 1));
                                 nh = bFragQ(imgH + an);
                                 nl = bFragQ(imgL + an);
                             }
@@ -539,7 +515,7 @@ __global__ __launch_bounds__(hxThreads<RB>()) void hx_kernel(HxArgs x, int nwc) 
                 }
                 if (nbar > 0) {
                     __syncthreads();  // partial slots of this macro period written
-                    for (int r = wt; r < x.nred; r += nwc) {
+                    for (int r = wt; r < x.nred; r += NW) {
                         const int* rt = x.reds + kBgRedInts * r;
                         const int rb = uni(rt[0]), n = uni(rt[1]);
                         f32x4 sum = *reinterpret_cast<const f32x4*>(pslots + static_cast<size_t>(uni(rt[2])) * 256 + lane * 4);
@@ -555,8 +531,18 @@ __global__ __launch_bounds__(hxThreads<RB>()) void hx_kernel(HxArgs x, int nwc) 
                 }
             }
         }
+        // block b2's quad maxima (its loads landed during the MFMA work)
+        if (more) {
+            hxMaskCols(x, items, b2, raw);
+            hxPublishMax(items, raw, lane, qeAll + 4 * ((it + 2) & 3));
+        }
+        // (the compiler cannot pair the two `more` branches: settle the items on the
+        // path it believes skips the publish, so the conversion above needs no wait)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+        for (int j = 0; j < kHxJ; ++j) asm volatile("" : "+v"(raw[j]));
     }
-    if (!(x.dbg & 8)) hxFixup(x, colExp + 32);
+    if (!(x.dbg & 8)) hxFixup(x, reinterpret_cast<int*>(qeAll + 16));
 }
 
 // Direct f32 FIR over outputs [od.o_lo, od.o_hi) x C channels (exact rows,

@@ -307,6 +307,7 @@ std::vector<int> HxPlan::progTable() const {
             e[5 + 4 * j] = sg.slot;
             e[6 + 4 * j] = 0;
         }
+        e[15] = rbMode ? kch * NS : pg.len;  // steps >= len (zero A) re-read rows [0, 32*(kch*NS - len))
     }
     return t;
 }
@@ -391,8 +392,11 @@ bool buildHxPlan(const FirPeriodic& f, HxPlan& plan) {
         const BgProg& pg = plan.progs[pi];
         for (int j = 0; j < pg.nseg; ++j) {
             const BgSeg& sg = pg.seg[j];
-            const int runLen = j == pg.nseg - 1 ? plen - sg.start : sg.ns;
+            // row-block mode runs the last segment on to plen; segmented mode
+            // points the padding steps at rows [0, 32*(plen - len))
+            const int runLen = j == pg.nseg - 1 && plan.rbMode ? plen - sg.start : sg.ns;
             plan.Kread = std::max(plan.Kread, sg.k0 + kHxStep * runLen);
+            if (!plan.rbMode) plan.Kread = std::max(plan.Kread, kHxStep * (plen - pg.len));
             for (int s = 0; s < sg.ns; ++s)
                 for (int lane = 0; lane < 64; ++lane) {
                     const int m = lane & 15, g = lane >> 4;

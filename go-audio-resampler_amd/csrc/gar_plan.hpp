@@ -90,11 +90,13 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
 // same permuted K order.
 // ---------------------------------------------------------------------------
 constexpr int kHxStep = 32;        // K per program step
-constexpr int kHxWaves = 8;        // segmented mode: compute waves per workgroup (+ 2 stager waves)
-constexpr int kHxMaxNS = 10;       // segmented mode register budget: 8 VGPRs of A per step (10 waves: 168 VGPRs)
-constexpr int kHxRbMaxWaves = 10;  // row-block mode: one compute wave per row block (+ 2 stagers: 3 waves/SIMD)
+constexpr int kHxWaves = 10;       // segmented mode: wave programs per workgroup
+constexpr int kHxMaxNS = 8;        // segmented mode register budget: 8 VGPRs of A per step (10 waves: 168 VGPRs)
+constexpr int kHxRbMaxWaves = 10;  // row-block mode: one wave per row block
 constexpr int kHxRbMaxNS = 10;     // row-block mode register budget (168 VGPRs)
-constexpr int kHxMaxRows = 1024;   // window rows per block: 16 per lane of a stager wave
+constexpr int kHxMaxRows = 1024;   // window rows per block (4*1024 staged items: 7 per lane at 10 waves)
+constexpr int kHxMinWaves = 10;    // waves per workgroup (waves past the programs only stage)
+constexpr int kHxMaxWaves = 10;    // __launch_bounds__ (3 waves per SIMD: 168 VGPRs)
 inline int hxPermK(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 struct HxPlan {
