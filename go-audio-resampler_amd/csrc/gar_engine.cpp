@@ -335,6 +335,7 @@ struct gar_resampler {
     bool profile = false;
     struct Ev { int tag; hipEvent_t a, b; };
     std::vector<Ev> events;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evPool;
     double profiledMs[4] = {0, 0, 0, 0};
     int64_t profiledLaunches[4] = {0, 0, 0, 0};
 };
@@ -355,8 +356,14 @@ struct Ctx {
 hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
     if (!x.h->profile) return launchBg(p, src, od, C, x.s);
     hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
+    if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
+        a = x.h->evPool.back().first;
+        b = x.h->evPool.back().second;
+        x.h->evPool.pop_back();
+    } else {
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+    }
     HIPCHK(hipEventRecord(a, x.s));
     const hipError_t e = launchBg(p, src, od, C, x.s);
     HIPCHK(hipEventRecord(b, x.s));
@@ -1002,6 +1009,14 @@ void gar_free(gar_resampler* r) {
     if (!r) return;
     try {
         if (r->stream) (void)hipStreamSynchronize(r->stream);
+        for (auto& ev : r->events) {
+            (void)hipEventDestroy(ev.a);
+            (void)hipEventDestroy(ev.b);
+        }
+        for (auto& ev : r->evPool) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
         r->groups.clear();
         r->stages.clear();
         if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -1195,6 +1210,20 @@ gar_status gar_flush_device(gar_resampler* r, void* out, int32_t out_dtype, int6
 void gar_reset(gar_resampler* r) {
     if (!r) return;
     try {
+        // one group over every channel: reset in place, keeping its device buffers
+        // (stream order covers kernels still reading them; no allocation, no sync)
+        if (r->groups.size() == 1 && r->groups[0].c0 == 0 && r->groups[0].C == r->channels) {
+            gar::Group& g = r->groups[0];
+            for (size_t i = 0; i < g.cnt.size(); ++i) {
+                g.cnt[i] = gar::Counters();
+                g.cnt[i].staged = !r->stages[i]->fused;
+            }
+            for (auto& d : g.dev) {
+                d.xh.clear();
+                d.uh.clear();
+            }
+            return;
+        }
         if (r->stream) (void)hipStreamSynchronize(r->stream);
         r->groups.clear();
         r->groups.push_back(freshGroup(r, 0, r->channels));
@@ -1267,8 +1296,7 @@ gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t*
             HIPCHK(hipEventElapsedTime(&t, ev.a, ev.b));
             r->profiledMs[ev.tag] += t;
             r->profiledLaunches[ev.tag] += 1;
-            (void)hipEventDestroy(ev.a);
-            (void)hipEventDestroy(ev.b);
+            r->evPool.emplace_back(ev.a, ev.b);
         }
         r->events.clear();
         if (ms) *ms = r->profiledMs[kind];

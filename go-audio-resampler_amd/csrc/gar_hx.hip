@@ -147,11 +147,11 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     x.rowMax = p.rowMax;
     x.zero = p.zero;
 
-    // edges first (they run while nothing else is queued), then the interior
-    hipError_t e = launchFir(p, src, od, od.o_lo, x.a0 * Pc, C, stream);
-    if (e != hipSuccess) return e;
-    e = launchFir(p, src, od, (a_lo + k1 * G) * Pc, od.o_hi, C, stream);
-    if (e != hipSuccess) return e;
+    // the launch edges run inside hx_kernel (spread over its waves before the blocks)
+    x.e0lo = od.o_lo;
+    x.e0hi = x.a0 * Pc;
+    x.e1lo = (a_lo + k1 * G) * Pc;
+    x.e1hi = od.o_hi;
 
     const size_t lds = ldsFor(G, parity);
     const int64_t blocks = std::min<int64_t>(x.nblocks, ncu);

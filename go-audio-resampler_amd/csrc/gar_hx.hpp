@@ -71,6 +71,7 @@ struct HxArgs {
     const int* rowLen;
     int rowMax;
     const float* zero;
+    int64_t e0lo, e0hi, e1lo, e1hi;  // launch edges [e0lo, e0hi) + [e1lo, e1hi): plain f32 FIR, spread over all waves
 };
 
 // ---- staging ----------------------------------------------------------------
@@ -331,6 +332,21 @@ __device__ __forceinline__ void hxFixup(const HxArgs& x, int* s_last) {
     }
 }
 
+// One output of the plain f32 FIR (exact rows, any source): lanes split the
+// taps, then a wave reduction.  Edges of hx launches and fir_kernel.
+__device__ __forceinline__ void firOne(const SrcDesc& src, const OutDesc& od, int64_t o, int c, int P, int Q,
+                                       const int* rowOff, const int* rowLen, const float* rows, int rowMax, int lane) {
+    const int64_t a = o / P;
+    const int r = static_cast<int>(o - a * P);
+    const int64_t t = a * Q + rowOff[r];
+    const float* row = rows + static_cast<size_t>(r) * rowMax;
+    float s = 0.f;
+    for (int k = lane; k < rowLen[r]; k += 64) s += row[k] * srcRead<float>(src, t + k, c);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) outWrite<float>(od, o, c, s);
+}
+
 template <int NS, bool RB, bool SINGLE>
 __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -374,6 +390,15 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     // work) and publishing its quad maxima at the end.  Exponent sets rotate
     // over 4 (block k uses set k & 3): iteration it reads sets it, it+1, writes
     // it+2 and zeroes it+3 (last read in iteration it-1).
+    {  // launch edges (history seam, partial chunks): one output per wave at a time
+        const int64_t n0 = (x.e0hi - x.e0lo) * x.C, n = n0 + (x.e1hi - x.e1lo) * x.C;
+        for (int64_t idx = static_cast<int64_t>(blockIdx.x) * NW + wt; idx < n; idx += static_cast<int64_t>(gridDim.x) * NW) {
+            const bool first = idx < n0;
+            const int64_t k = first ? idx : idx - n0;
+            const int64_t o = (first ? x.e0lo : x.e1lo) + k / x.C;
+            firOne(x.src, x.od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, x.rowOff, x.rowLen, x.rows, x.rowMax, lane);
+        }
+    }
     const HxItems items = hxItems(x.Ws, wt, NW);
     f32x4 raw[kHxJ];
     if (threadIdx.x < 16) qeAll[threadIdx.x] = 0;
@@ -554,19 +579,8 @@ __global__ __launch_bounds__(256) void fir_kernel(SrcDesc src, OutDesc od, int C
     const int lane = threadIdx.x & 63;
     const int64_t n = (od.o_hi - od.o_lo) * C;
     const int64_t wstep = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
-    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); idx < n; idx += wstep) {
-        const int64_t o = od.o_lo + idx / C;
-        const int c = static_cast<int>(idx % C);
-        const int64_t a = o / P;
-        const int r = static_cast<int>(o - a * P);
-        const int64_t t = a * Q + rowOff[r];
-        const float* row = rows + static_cast<size_t>(r) * rowMax;
-        float s = 0.f;
-        for (int k = lane; k < rowLen[r]; k += 64) s += row[k] * srcRead<float>(src, t + k, c);
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-        if (lane == 0) outWrite<float>(od, o, c, s);
-    }
+    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); idx < n; idx += wstep)
+        firOne(src, od, od.o_lo + idx / C, static_cast<int>(idx % C), P, Q, rowOff, rowLen, rows, rowMax, lane);
 }
 
 }  // namespace gar
