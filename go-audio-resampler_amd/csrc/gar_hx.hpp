@@ -78,7 +78,7 @@ struct HxArgs {
 // Image buffer layout: quad q (columns 4q..4q+3) at q*QS, QS = 16*Ws + 64: hi
 // rows (4 f16 = 8 B each) then lo rows; the +64 B skew puts the four quads of
 // any 8 consecutive rows on distinct banks for ds_read_b64_tr_b16.
-// Items: the block's 4*Ws (quad, row) pairs; item t = (wave + NW*j)*64 + lane
+// Items: the block's 4*Ws (quad, row) pairs; item t = (wave*kHxJ + j)*64 + lane
 // for j < kHxJ, so each wave-instruction's 64 items are 64 consecutive rows of
 // one quad (Ws % 64 == 0) and its loads coalesce.  Rows >= W are clamped to
 // row W-1 (finite; A is zero there); columns past the launch read zeros.
@@ -89,17 +89,21 @@ struct HxItems {
     int r0[kHxJ];    // first row of the slot's 64 rows
 };
 
-__device__ __forceinline__ HxItems hxItems(int Ws, int wt, int NW) {
+__device__ __forceinline__ HxItems hxItems(int Ws, int wt) {
     HxItems it;
 #pragma unroll
     for (int j = 0; j < kHxJ; ++j) {
-        const int tb = (wt + NW * j) * 64;
+        const int tb = (wt * kHxJ + j) * 64;  // a wave's slots are contiguous: they span <= 2 quads (Ws >= 448)
         const int q = tb < 4 * Ws ? tb / Ws : -1;
         it.q[j] = uni(q);
         it.r0[j] = uni(q >= 0 ? tb - q * Ws : 0);
     }
     return it;
 }
+
+#define GAR_HX_SLOTS(it)                                                         \
+    _Pragma("unroll") for (int j = 0, q = (it).q[0], r = (it).r0[0]; j < kHxJ; \
+                           ++j, q = j < kHxJ ? (it).q[j] : -1, r = j < kHxJ ? (it).r0[j] : 0) if (q >= 0)
 
 // Raw buffer loads: a wave-uniform resource (SGPRs) per chunk/column base and a
 // 32-bit lane offset; the compiler tracks them as loads (vmcnt) and keeps the
@@ -113,11 +117,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t hxRsrc(const float* base) {
 // chunk and are zeroed afterwards), so no branch separates a load from its use.
 __device__ __forceinline__ void hxLoad(const HxArgs& x, const HxItems& it, int bl, int lane, f32x4 (&v)[kHxJ]) {
     const uint32_t fsB = static_cast<uint32_t>(x.in_fs) * 4u;
-#pragma unroll
-    for (int j = 0; j < kHxJ; ++j) {
-        if (it.q[j] < 0) continue;
-        const int off = static_cast<int>(static_cast<uint32_t>(min(it.r0[j] + lane, x.W - 1)) * fsB);
-        const int col = bl * 16 + 4 * it.q[j];
+    GAR_HX_SLOTS(it) {
+        const int off = static_cast<int>(static_cast<uint32_t>(min(r + lane, x.W - 1)) * fsB);
+        const int col = bl * 16 + 4 * q;
         if (x.fmt == 1) {  // stereo frames: chunks col/2 and col/2 + 1, both channels
             const int ck0 = col < x.ncols ? col >> 1 : 0, ck1 = col + 2 < x.ncols ? (col >> 1) + 1 : 0;
             const f2v a = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(
@@ -143,10 +145,8 @@ __device__ __forceinline__ void hxLoad(const HxArgs& x, const HxItems& it, int b
 
 // Zero the lanes of item slots whose columns lie past the launch (after the loads landed).
 __device__ __forceinline__ void hxMaskCols(const HxArgs& x, const HxItems& it, int bl, f32x4 (&v)[kHxJ]) {
-#pragma unroll
-    for (int j = 0; j < kHxJ; ++j) {
-        if (it.q[j] < 0) continue;
-        const int col = bl * 16 + 4 * it.q[j];
+    GAR_HX_SLOTS(it) {
+        const int col = bl * 16 + 4 * q;
         if (col + 4 <= x.ncols) continue;  // uniform: whole quad inside
 #pragma unroll
         for (int n = 0; n < 4; ++n)
@@ -175,16 +175,20 @@ __device__ __forceinline__ void hxPublishMax(const HxItems& it, f32x4 (&v)[kHxJ]
     __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
     for (int j = 0; j < kHxJ; ++j) asm volatile("" : "+v"(v[j]));
-#pragma unroll
-    for (int j = 0; j < kHxJ; ++j) {
-        if (it.q[j] < 0) continue;
+    // running lane max over consecutive slots of one quad; one wave reduction +
+    // LDS atomic per quad the wave touches
+    uint32_t run = 0;
+    GAR_HX_SLOTS(it) {
         const f2v v01 = {v[j][0], v[j][1]}, v23 = {v[j][2], v[j][3]};
         const f2v nacc = __builtin_elementwise_fma(v23, z, __builtin_elementwise_fma(v01, z, z));
         const float m = fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])), fmaxf(fabsf(v[j][2]), fabsf(v[j][3])));
-        uint32_t mu = __float_as_uint(m);
-        if (!(nacc.x == 0.f && nacc.y == 0.f)) mu = 0x7f800000u;
-        mu = hxWaveMax(mu);
-        if (lane == 0) atomicMax(qe + it.q[j], mu);
+        const uint32_t mu = (nacc.x == 0.f && nacc.y == 0.f) ? __float_as_uint(m) : 0x7f800000u;
+        run = max(run, mu);
+        if (j + 1 == kHxJ || it.q[j + 1] != q) {  // uniform: last slot of this quad
+            const uint32_t w = hxWaveMax(run);
+            if (lane == 0) atomicMax(qe + q, w);
+            run = 0;
+        }
     }
 }
 
@@ -216,14 +220,25 @@ __device__ __forceinline__ void hxPutRow(char* qb, int Ws, int r, f2v sc, f2v v0
 __device__ __forceinline__ void hxConvert(const HxItems& it, const f32x4 (&v)[kHxJ], int Ws, int lane, char* buf,
                                           const uint32_t* qe) {
     const uint32_t QS = hxQS(Ws);
+    // quad exponents once (uniform), then per slot a scalar select
+    int e4[4];
 #pragma unroll
-    for (int j = 0; j < kHxJ; ++j) {
-        if (it.q[j] < 0) continue;
-        const int e = hxExpOf(qe[it.q[j]]);
+    for (int q = 0; q < 4; ++q) e4[q] = uni(hxExpOf(qe[q]));
+    GAR_HX_SLOTS(it) {
+        const int e = q == 0 ? e4[0] : q == 1 ? e4[1] : q == 2 ? e4[2] : e4[3];
         if (e == kHxNonFinite) continue;  // block is recomputed by the slow path
         const float s1 = __uint_as_float(static_cast<uint32_t>(e + 127) << 23);
-        hxPutRow(buf + it.q[j] * QS, Ws, it.r0[j] + lane, f2v{s1, s1}, f2v{v[j][0], v[j][1]}, f2v{v[j][2], v[j][3]});
+        hxPutRow(buf + q * QS, Ws, r + lane, f2v{s1, s1}, f2v{v[j][0], v[j][1]}, f2v{v[j][2], v[j][3]});
     }
+}
+
+// (same, from a 32-bit LDS byte address: base + constant offsets fold into the
+// instruction's offset field)
+__device__ __forceinline__ h8v bFragA(uint32_t a) {
+    const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4p)(a));
+    const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4p)(a + 128));
+    const s8v v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(h8v, v);
 }
 
 // B fragment (32 K x 16 columns) at the lane's transposed-read address p:
@@ -249,7 +264,9 @@ __device__ __forceinline__ void hxPut4(const HxArgs& x, char* p, f32x4 y, int la
     if (x.vst == 2) {
         const bool even = (lane & 1) == 0;
         const float s0 = even ? y[2] : y[0], s1 = even ? y[3] : y[1];
-        const float q0 = __shfl_xor(s0, 1), q1 = __shfl_xor(s1, 1);
+        // lane ^ 1 (DPP quad_perm [1,0,3,2]: no LDS round trip)
+        const float q0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xf, 0xf, false));
+        const float q1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xf, 0xf, false));
         f32x4 w;
         if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
         else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
@@ -399,7 +416,7 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
             firOne(x.src, x.od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, x.rowOff, x.rowLen, x.rows, x.rowMax, lane);
         }
     }
-    const HxItems items = hxItems(x.Ws, wt, NW);
+    const HxItems items = hxItems(x.Ws, wt);
     f32x4 raw[kHxJ];
     if (threadIdx.x < 16) qeAll[threadIdx.x] = 0;
     int b = blockIdx.x;
@@ -454,40 +471,66 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
                                   : x.out + chunk * x.out_chunk + c * x.out_cs + (rbw * 16 + 4 * grp) * x.out_fs;
                 const int64_t ostep = static_cast<int64_t>(x.Pc) * x.out_fs;
                 // the wave's step stream: element u = step u % NS of period u / NS at
-                // rows gi*Qc + u0 + 32 s (+8 B per row); B runs one element ahead,
-                // across periods (reads past the last period land inside LDS, unused)
+                // rows gi*Qc + u0 + 32 s (+8 B per row); B is read one element ahead,
+                // across periods (reads past the last period land inside LDS, unused).
+                // Three accumulators (one per product term): no MFMA waits on the one
+                // before it.
                 const uint32_t gstep = 8u * static_cast<uint32_t>(x.Qc);
-                const char* ph = imgH + 8u * static_cast<uint32_t>(u0);
-                const char* pl = imgL + 8u * static_cast<uint32_t>(u0);
-                h8v bh0 = bFragQ(ph), bl0 = bFragQ(pl);
-                for (int gi = 0; gi < x.G; ++gi) {
-                    f32x4 accB = {0, 0, 0, 0}, accS = accB;
-#pragma unroll
-                    for (int s = 0; s < NS; ++s) {
-                        const char* nh = s + 1 < NS ? ph + 256 * (s + 1) : ph + gstep;
-                        const char* nl = s + 1 < NS ? pl + 256 * (s + 1) : pl + gstep;
-                        const h8v bh1 = bFragQ(nh), bl1 = bFragQ(nl);
-                        accB = mfma16(Ah[s], bh0, accB);
-                        accS = mfma16(Ah[s], bl0, accS);
-                        accS = mfma16(Al[s], bh0, accS);
-                        bh0 = bh1; bl0 = bl1;
-                        __builtin_amdgcn_sched_barrier(0);  // keep reads(s + 1) -> MFMAs(s) order per step
-                    }
-                    ph += gstep;
-                    pl += gstep;
-                    const f32x4 y = hxScale(accB + accS, sh);
+                const uint32_t dL = 8u * static_cast<uint32_t>(x.Ws);
+                uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)imgH)) + 8u * static_cast<uint32_t>(u0);
+                h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
+                // epilogue of one period: scale, store (the previous period's, issued
+                // from inside the next period's MFMA stream so the waves' MFMA pipes
+                // never idle through it)
+                auto epilogue = [&](const f32x4& oA, char* ep) {
+                    const f32x4 y = hxScale(oA, sh);
                     if (full) {
-                        if (colOk) hxPut4(x, optr, y, lane);
+                        if (colOk) hxPut4(x, ep, y, lane);
                     } else {  // partial last row block: rows < Pc only
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
                             if (colOk && rbw * 16 + 4 * grp + i < x.Pc) {
-                                char* pp = optr + i * x.out_fs;
+                                char* pp = ep + i * x.out_fs;
                                 if (x.out_f64) *reinterpret_cast<double*>(pp) = y[i];
                                 else *reinterpret_cast<float*>(pp) = y[i];
                             }
                     }
-                    optr += ostep;
+                };
+                // one period's MFMA program into nA (one accumulator for the three
+                // product terms); the epilogue of oA at ep runs after its first step when epi
+                auto period = [&](f32x4& nA, const f32x4& oA, bool epi, char* ep) {
+                    asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
+                    const uint32_t aL = aH + dL, aN = aH + gstep, aNL = aN + dL;
+                    nA = f32x4{0, 0, 0, 0};
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) {
+                        const int ug = (s + 1) / NS, us = (s + 1) % NS;
+                        const h8v bh1 = bFragA((ug == 0 ? aH : aN) + 256 * us);
+                        const h8v bl1 = bFragA((ug == 0 ? aL : aNL) + 256 * us);
+                        nA = mfma16(Ah[s], bh0, nA);
+                        nA = mfma16(Al[s], bh0, nA);
+                        nA = mfma16(Ah[s], bl0, nA);
+                        bh0 = bh1; bl0 = bl1;
+                        // per step: the 4 LDS reads issue first, then the 3 MFMAs; nothing crosses steps
+                        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (s == (NS > 1 ? 1 : 0) && epi) epilogue(oA, ep);
+                    }
+                    aH = aN;
+                };
+                f32x4 a0, a1 = {0, 0, 0, 0};
+                int gi = 0;
+                for (; gi + 1 < x.G; gi += 2) {  // periods in pairs: alternating accumulators
+                    period(a0, a1, gi > 0, optr - ostep);
+                    period(a1, a0, true, optr);
+                    optr += 2 * ostep;
+                }
+                if (gi < x.G) {
+                    period(a0, a1, gi > 0, optr - ostep);
+                    epilogue(a0, optr);
+                } else {
+                    epilogue(a1, optr - ostep);
                 }
             }
         } else {

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libgar.so")
+LIB_PATH = os.environ.get("GAR_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "libgar.so")  # override: A/B builds
 
 # resampler.QualityPreset (resample.go:104-131)
 QualityQuick, QualityLow, QualityMedium, QualityHigh, QualityVeryHigh, QualityCustom = range(6)
