@@ -124,7 +124,7 @@ bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry) {
         d.rowOff = static_cast<const int*>(h.roff.p);
         d.rowLen = static_cast<const int*>(h.rlen.p);
         d.fixCap = 4096;
-        h.fix.upload(std::vector<int>(2 + d.fixCap + 64, 0));
+        h.fix.upload(std::vector<int>(2 + d.fixCap + 64 + 256, 0));  // list, 64 zero words, 1 KiB store sink
         d.fix = static_cast<int*>(h.fix.p);
         d.zero = reinterpret_cast<const float*>(d.fix + 2 + d.fixCap);  // 64 zero words past the list
     }

@@ -10,27 +10,38 @@
 
 namespace gar {
 
+// hxLaunch instantiations live in gar_hx_i*.hip (compiled in parallel)
+#define GAR_HX_EXTERN(NS, RB, V) \
+    extern template hipError_t hxLaunch<NS, RB, V>(const HxArgs&, int, size_t, int64_t, hipStream_t);
+GAR_HX_FOR_ALL(GAR_HX_EXTERN)
+#undef GAR_HX_EXTERN
+
+// Direct f32 FIR over outputs [od.o_lo, od.o_hi) x C channels (exact rows,
+// any source): the edges of a launch (history seam, flush zeros, partial
+// macro periods) and launches too small for hx_kernel.  One wave per output:
+// lanes split the taps, then a wave reduction.
+__global__ __launch_bounds__(256) void fir_kernel(SrcDesc src, OutDesc od, int C, int P, int Q, const int* rowOff,
+                                                  const int* rowLen, const float* rows, int rowMax) {
+    const int lane = threadIdx.x & 63;
+    const int64_t n = (od.o_hi - od.o_lo) * C;
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
+    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); idx < n; idx += wstep)
+        firOne(src, od, od.o_lo + idx / C, static_cast<int>(idx % C), P, Q, rowOff, rowLen, rows, rowMax, lane);
+}
+
 namespace {
 
+
+// row-block mode: the epilogue store layout (HxArgs::vst) is a template parameter
 template <int NS, bool RB>
 hipError_t hxDispatch(const HxArgs& x, int waves, size_t lds, int64_t blocks, hipStream_t st) {
-    static bool attrSet = false;
-    if (!attrSet) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if constexpr (!RB)
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attrSet = true;
+    if constexpr (!RB) return hxLaunch<NS, false, 0>(x, waves, lds, blocks, st);
+    switch (x.vst) {
+        case 0: return hxLaunch<NS, RB, 0>(x, waves, lds, blocks, st);
+        case 1: return hxLaunch<NS, RB, 1>(x, waves, lds, blocks, st);
+        case 2: return hxLaunch<NS, RB, 2>(x, waves, lds, blocks, st);
+        default: return hxLaunch<NS, RB, 3>(x, waves, lds, blocks, st);
     }
-    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * waves);
-    if constexpr (RB) {
-        hipLaunchKernelGGL((hx_kernel<NS, true, true>), gd, bd, lds, st, x);
-    } else {
-        if (x.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, false, true>), gd, bd, lds, st, x);
-        else hipLaunchKernelGGL((hx_kernel<NS, false, false>), gd, bd, lds, st, x);
-    }
-    return hipGetLastError();
 }
 
 hipError_t launchFir(const HxDev& p, const SrcDesc& src, OutDesc od, int64_t lo, int64_t hi, int C, hipStream_t st) {

@@ -85,25 +85,24 @@ struct HxArgs {
 __device__ __forceinline__ uint32_t hxQS(int Ws) { return 16u * static_cast<uint32_t>(Ws) + 64u; }
 
 struct HxItems {
-    int q[kHxJ];     // quad of item slot j (wave-uniform), -1: none
-    int r0[kHxJ];    // first row of the slot's 64 rows
+    int n0;          // global index of the wave's slot 0 (slot j covers rows 64*(n0+j) .. of the flattened quads)
+    int d, inv;      // Ws/64 and ceil(2^16/d): q = (n*inv) >> 16 exactly for n < 2^10
+    int nmax;        // 4*d slots in the block
 };
 
 __device__ __forceinline__ HxItems hxItems(int Ws, int wt) {
     HxItems it;
-#pragma unroll
-    for (int j = 0; j < kHxJ; ++j) {
-        const int tb = (wt * kHxJ + j) * 64;  // a wave's slots are contiguous: they span <= 2 quads (Ws >= 448)
-        const int q = tb < 4 * Ws ? tb / Ws : -1;
-        it.q[j] = uni(q);
-        it.r0[j] = uni(q >= 0 ? tb - q * Ws : 0);
-    }
+    it.n0 = uni(wt * kHxJ);
+    it.d = uni(Ws >> 6);
+    it.inv = uni((65536 + it.d - 1) / it.d);
+    it.nmax = 4 * it.d;
     return it;
 }
 
-#define GAR_HX_SLOTS(it)                                                         \
-    _Pragma("unroll") for (int j = 0, q = (it).q[0], r = (it).r0[0]; j < kHxJ; \
-                           ++j, q = j < kHxJ ? (it).q[j] : -1, r = j < kHxJ ? (it).r0[j] : 0) if (q >= 0)
+// Walks a wave's slots j = 0..kHxJ-1: quad q and first row r (wave-uniform scalars).
+#define GAR_HX_SLOTS(it)                                                                                  \
+    _Pragma("unroll") for (int j = 0, n = (it).n0, q = (n * (it).inv) >> 16, r = 64 * (n - q * (it).d); \
+                           j < kHxJ; ++j, n = (it).n0 + j, q = (n * (it).inv) >> 16, r = 64 * (n - q * (it).d)) if (n < (it).nmax)
 
 // Raw buffer loads: a wave-uniform resource (SGPRs) per chunk/column base and a
 // 32-bit lane offset; the compiler tracks them as loads (vmcnt) and keeps the
@@ -116,28 +115,34 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t hxRsrc(const float* base) {
 // Every slot loads unconditionally (columns past the launch read column 0's
 // chunk and are zeroed afterwards), so no branch separates a load from its use.
 __device__ __forceinline__ void hxLoad(const HxArgs& x, const HxItems& it, int bl, int lane, f32x4 (&v)[kHxJ]) {
+    // one buffer resource per block (its first chunk); per slot a scalar byte
+    // offset (chunk, channel) and the lane's row offset
     const uint32_t fsB = static_cast<uint32_t>(x.in_fs) * 4u;
+    const uint32_t chB = static_cast<uint32_t>(x.in_chunk) * 4u, csB = static_cast<uint32_t>(x.in_cs) * 4u;
+    const int ckB = uni((bl * 16) / x.C);
+    const __amdgpu_buffer_rsrc_t rs = hxRsrc(x.in + static_cast<int64_t>(ckB) * x.in_chunk);
     GAR_HX_SLOTS(it) {
         const int off = static_cast<int>(static_cast<uint32_t>(min(r + lane, x.W - 1)) * fsB);
         const int col = bl * 16 + 4 * q;
         if (x.fmt == 1) {  // stereo frames: chunks col/2 and col/2 + 1, both channels
-            const int ck0 = col < x.ncols ? col >> 1 : 0, ck1 = col + 2 < x.ncols ? (col >> 1) + 1 : 0;
-            const f2v a = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(
-                                                      hxRsrc(x.in + static_cast<int64_t>(ck0) * x.in_chunk), off, 0, 0));
-            const f2v c = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(
-                                                      hxRsrc(x.in + static_cast<int64_t>(ck1) * x.in_chunk), off, 0, 0));
+            const int k0 = (col >> 1) - ckB;
+            const int s0 = col < x.ncols ? static_cast<int>(k0 * chB) : 0;
+            const int s1 = col + 2 < x.ncols ? static_cast<int>((k0 + 1) * chB) : 0;
+            const f2v a = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, off, s0, 0));
+            const f2v c = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, off, s1, 0));
             v[j] = f32x4{a.x, a.y, c.x, c.y};
         } else if (x.fmt == 2) {  // four contiguous channels of one chunk
-            const int cc = col < x.ncols ? col : 0;
+            const int cc = col < x.ncols ? col : bl * 16;
             const int ck = cc / x.C, c0 = cc - ck * x.C;
-            v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hxRsrc(x.in + ck * x.in_chunk + c0), off, 0, 0));
+            const int so = static_cast<int>((ck - ckB) * chB + c0 * 4u);
+            v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, so, 0));
         } else {
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
-                const int cn = col + n < x.ncols ? col + n : 0;
+                const int cn = col + n < x.ncols ? col + n : bl * 16;
                 const int ck = cn / x.C, c = cn - ck * x.C;
-                v[j][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                         hxRsrc(x.in + ck * x.in_chunk + c * x.in_cs), off, 0, 0));
+                const int so = static_cast<int>((ck - ckB) * chB + c * csB);
+                v[j][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, off, so, 0));
             }
         }
     }
@@ -184,7 +189,7 @@ __device__ __forceinline__ void hxPublishMax(const HxItems& it, f32x4 (&v)[kHxJ]
         const float m = fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])), fmaxf(fabsf(v[j][2]), fabsf(v[j][3])));
         const uint32_t mu = (nacc.x == 0.f && nacc.y == 0.f) ? __float_as_uint(m) : 0x7f800000u;
         run = max(run, mu);
-        if (j + 1 == kHxJ || it.q[j + 1] != q) {  // uniform: last slot of this quad
+        if (j + 1 == kHxJ || n + 1 >= it.nmax || r + 64 >= 64 * it.d) {  // uniform: last slot of this quad
             const uint32_t w = hxWaveMax(run);
             if (lane == 0) atomicMax(qe + q, w);
             run = 0;
@@ -241,6 +246,19 @@ __device__ __forceinline__ h8v bFragA(uint32_t a) {
     return __builtin_bit_cast(h8v, v);
 }
 
+// Slot j of hxConvert (exponents e4 already decoded); for conversion spread
+// over the MFMA steps.
+__device__ __forceinline__ void hxConvertSlot(const HxItems& it, const f32x4 (&v)[kHxJ], int j, const int (&e4)[4],
+                                              int Ws, int lane, char* buf) {
+    const int n = it.n0 + j;
+    if (n >= it.nmax) return;
+    const int q = (n * it.inv) >> 16, r = 64 * (n - q * it.d);
+    const int e = q == 0 ? e4[0] : q == 1 ? e4[1] : q == 2 ? e4[2] : e4[3];
+    if (e == kHxNonFinite) return;
+    const float s1 = __uint_as_float(static_cast<uint32_t>(e + 127) << 23);
+    hxPutRow(buf + q * hxQS(Ws), Ws, r + lane, f2v{s1, s1}, f2v{v[j][0], v[j][1]}, f2v{v[j][2], v[j][3]});
+}
+
 // B fragment (32 K x 16 columns) at the lane's transposed-read address p:
 // lane 16g + 4qr + qd supplies row 4g + qr (and +16) of quad qd.
 __device__ __forceinline__ h8v bFragQ(const char* p) {
@@ -260,8 +278,9 @@ __device__ __forceinline__ f32x4 hxScale(f32x4 r, int sh) {
 //  vst 2: stereo interleaved f32 (lanes n, n^1 = channels 0/1 swap halves: one 16-B store of two frames each)
 //  vst 1: channel-contiguous f32 (one 16-B store)
 //  vst 0: any other f32 layout (4 stores);  vst 3: f64 output (4 stores)
+template <int VST>
 __device__ __forceinline__ void hxPut4(const HxArgs& x, char* p, f32x4 y, int lane) {
-    if (x.vst == 2) {
+    if (VST == 2) {
         const bool even = (lane & 1) == 0;
         const float s0 = even ? y[2] : y[0], s1 = even ? y[3] : y[1];
         // lane ^ 1 (DPP quad_perm [1,0,3,2]: no LDS round trip)
@@ -271,9 +290,9 @@ __device__ __forceinline__ void hxPut4(const HxArgs& x, char* p, f32x4 y, int la
         if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
         else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
         *reinterpret_cast<f32x4*>(p) = w;
-    } else if (x.vst == 1) {
+    } else if (VST == 1) {
         *reinterpret_cast<f32x4*>(p) = y;
-    } else if (x.vst == 0) {
+    } else if (VST == 0) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
     } else {
@@ -349,6 +368,22 @@ __device__ __forceinline__ void hxFixup(const HxArgs& x, int* s_last) {
     }
 }
 
+// The kernel's argument block behind an opaque pointer: fields the cold paths
+// (edges, non-finite fixup) read through it are loaded where used, instead of
+// being hoisted to the kernel entry and held in SGPRs across the block loop.
+typedef const __attribute__((address_space(4))) HxArgs* HxArgsK;
+template <class T>
+__device__ __forceinline__ T kload(const __attribute__((address_space(4))) T* p) {
+    T v;
+    __builtin_memcpy(&v, (const T*)p, sizeof(T));
+    return v;
+}
+__device__ __forceinline__ HxArgsK hxCold() {
+    uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(v));
+    return reinterpret_cast<HxArgsK>(v);
+}
+
 // One output of the plain f32 FIR (exact rows, any source): lanes split the
 // taps, then a wave reduction.  Edges of hx launches and fir_kernel.
 __device__ __forceinline__ void firOne(const SrcDesc& src, const OutDesc& od, int64_t o, int c, int P, int Q,
@@ -364,7 +399,7 @@ __device__ __forceinline__ void firOne(const SrcDesc& src, const OutDesc& od, in
     if (lane == 0) outWrite<float>(od, o, c, s);
 }
 
-template <int NS, bool RB, bool SINGLE>
+template <int NS, bool RB, bool SINGLE, int VST>
 __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t QS = hxQS(x.Ws);
@@ -413,7 +448,10 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
             const bool first = idx < n0;
             const int64_t k = first ? idx : idx - n0;
             const int64_t o = (first ? x.e0lo : x.e1lo) + k / x.C;
-            firOne(x.src, x.od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, x.rowOff, x.rowLen, x.rows, x.rowMax, lane);
+            const HxArgsK xc = hxCold();
+            const SrcDesc src = kload(&xc->src);
+            const OutDesc od = kload(&xc->od);
+            firOne(src, od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, xc->rowOff, xc->rowLen, xc->rows, xc->rowMax, lane);
         }
     }
     const HxItems items = hxItems(x.Ws, wt);
@@ -441,16 +479,28 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
         const uint32_t* qeCur = qeAll + 4 * (it & 3);
         if (threadIdx.x < 4) qeAll[4 * ((it + 3) & 3) + threadIdx.x] = 0;
         const int b1 = b + G2, b2 = b1 + G2;
-        if (b1 < x.nblocks && staging)
-            hxConvert(items, raw, x.Ws, lane, imgs + static_cast<size_t>((it + 1) & 1) * bufB, qeAll + 4 * ((it + 1) & 3));
+        const bool conv = b1 < x.nblocks && staging;
         const bool more = b2 < x.nblocks && staging;
-        if (more) hxLoad(x, items, b2, lane, raw);
+        char* bufN = imgs + static_cast<size_t>((it + 1) & 1) * bufB;
+        const int myE = hxExpOf(qeCur[l16 >> 2]);
+        const bool nonFinite = __any(myE == kHxNonFinite);
+        // row-block waves convert block b1's slots inside their first period's MFMA
+        // steps and issue block b2's loads after it; everyone else does it here
+        const bool convInLoop = RB && nseg > 0 && !(x.dbg & 2) && !nonFinite;
+        int e4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e4[k] = uni(hxExpOf(qeAll[4 * ((it + 1) & 3) + k]));
+        if (!convInLoop) {
+            if (conv) {
+#pragma unroll
+                for (int j = 0; j < kHxJ; ++j) hxConvertSlot(items, raw, j, e4, x.Ws, lane, bufN);
+            }
+            if (more) hxLoad(x, items, b2, lane, raw);
+        }
 
         const int cur = it & 1;
         const char* imgH = imgs + static_cast<size_t>(cur) * bufB + laneOff;
         const char* imgL = imgH + 8 * x.Ws;
-        const int myE = hxExpOf(qeCur[l16 >> 2]);
-        const bool nonFinite = __any(myE == kHxNonFinite);
         const int sh = -(x.ea + myE);
         const int col = b * 16 + l16;
         const bool colOk = col < x.ncols;
@@ -458,8 +508,10 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
 
         if (nonFinite) {
             if (wt == 0 && lane == 0) {
-                const int k = atomicAdd(&x.fix[0], 1);
-                if (k < x.fixCap) x.fix[2 + k] = b;
+                const HxArgsK xc = hxCold();
+                int* fix = xc->fix;
+                const int k = atomicAdd(&fix[0], 1);
+                if (k < xc->fixCap) fix[2 + k] = b;
             }
             for (int gi = 0; gi < x.G; ++gi, ++q)
                 for (int k = 0; k < nbar; ++k) __syncthreads();
@@ -484,8 +536,11 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
                 // never idle through it)
                 auto epilogue = [&](const f32x4& oA, char* ep) {
                     const f32x4 y = hxScale(oA, sh);
+#ifdef GAR_HX_NOEPI
+                    if (!(x.dbg & 4096)) return;  // (experiment: no epilogue stores)
+#endif
                     if (full) {
-                        if (colOk) hxPut4(x, ep, y, lane);
+                        if (colOk) hxPut4<VST>(x, ep, y, lane);
                     } else {  // partial last row block: rows < Pc only
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
@@ -498,7 +553,7 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
                 };
                 // one period's MFMA program into nA (one accumulator for the three
                 // product terms); the epilogue of oA at ep runs after its first step when epi
-                auto period = [&](f32x4& nA, const f32x4& oA, bool epi, char* ep) {
+                auto period = [&](f32x4& nA, const f32x4& oA, bool epi, char* ep, bool first) {
                     asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
                     const uint32_t aL = aH + dL, aN = aH + gstep, aNL = aN + dL;
                     nA = f32x4{0, 0, 0, 0};
@@ -516,21 +571,30 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
                         __builtin_amdgcn_sched_barrier(0);
                         if (s == (NS > 1 ? 1 : 0) && epi) epilogue(oA, ep);
+                        if (first && conv) {  // block b1's slots j = s, s + NS, ...
+#pragma unroll
+                            for (int j = s; j < kHxJ; j += NS) hxConvertSlot(items, raw, j, e4, x.Ws, lane, bufN);
+                        }
                     }
                     aH = aN;
                 };
                 f32x4 a0, a1 = {0, 0, 0, 0};
-                int gi = 0;
+                // period 0 also converts block b1; block b2's loads follow it and land
+                // during the remaining periods
+                period(a0, a1, false, optr, true);
+                if (more) hxLoad(x, items, b2, lane, raw);
+                int gi = 1;
                 for (; gi + 1 < x.G; gi += 2) {  // periods in pairs: alternating accumulators
-                    period(a0, a1, gi > 0, optr - ostep);
-                    period(a1, a0, true, optr);
-                    optr += 2 * ostep;
+                    period(a1, a0, true, optr, false);
+                    optr += ostep;
+                    period(a0, a1, true, optr, false);
+                    optr += ostep;
                 }
                 if (gi < x.G) {
-                    period(a0, a1, gi > 0, optr - ostep);
-                    epilogue(a0, optr);
+                    period(a1, a0, true, optr, false);
+                    epilogue(a1, optr + ostep);
                 } else {
-                    epilogue(a1, optr - ostep);
+                    epilogue(a0, optr);
                 }
             }
         } else {
@@ -610,20 +674,44 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
 #pragma unroll
         for (int j = 0; j < kHxJ; ++j) asm volatile("" : "+v"(raw[j]));
     }
-    if (!(x.dbg & 8)) hxFixup(x, reinterpret_cast<int*>(qeAll + 16));
+    if (!(x.dbg & 8)) {
+        const HxArgs xc = kload(hxCold());
+        hxFixup(xc, reinterpret_cast<int*>(qeAll + 16));
+    }
 }
 
-// Direct f32 FIR over outputs [od.o_lo, od.o_hi) x C channels (exact rows,
-// any source): the edges of a launch (history seam, flush zeros, partial
-// macro periods) and launches too small for hx_kernel.  One wave per output:
-// lanes split the taps, then a wave reduction.
-__global__ __launch_bounds__(256) void fir_kernel(SrcDesc src, OutDesc od, int C, int P, int Q, const int* rowOff,
-                                                  const int* rowLen, const float* rows, int rowMax) {
-    const int lane = threadIdx.x & 63;
-    const int64_t n = (od.o_hi - od.o_lo) * C;
-    const int64_t wstep = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
-    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x >> 6) + (threadIdx.x >> 6); idx < n; idx += wstep)
-        firOne(src, od, od.o_lo + idx / C, static_cast<int>(idx % C), P, Q, rowOff, rowLen, rows, rowMax, lane);
+// Direct f32 FIR (launch edges too small for hx_kernel); defined in gar_hx.hip.
+__global__ void fir_kernel(SrcDesc src, OutDesc od, int C, int P, int Q, const int* rowOff, const int* rowLen,
+                           const float* rows, int rowMax);
+
+// Launch of one hx_kernel instantiation (explicitly instantiated in gar_hx_i*.hip).
+template <int NS, bool RB, int VST>
+hipError_t hxLaunch(const HxArgs& x, int waves, size_t lds, int64_t blocks, hipStream_t st) {
+    static bool attrSet = false;
+    if (!attrSet) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, true, VST>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if constexpr (!RB)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hx_kernel<NS, RB, false, VST>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attrSet = true;
+    }
+    const dim3 gd(static_cast<unsigned>(blocks)), bd(64 * waves);
+    if constexpr (RB) {
+        hipLaunchKernelGGL((hx_kernel<NS, true, true, VST>), gd, bd, lds, st, x);
+    } else {
+        if (x.kch == 1) hipLaunchKernelGGL((hx_kernel<NS, false, true, VST>), gd, bd, lds, st, x);
+        else hipLaunchKernelGGL((hx_kernel<NS, false, false, VST>), gd, bd, lds, st, x);
+    }
+    return hipGetLastError();
 }
+
+// every instantiation launchHx can reach: RB NS 1..10 x store layouts 0..3, SEG NS 2..8 (even)
+#define GAR_HX_FOR_RB(M, NS) M(NS, true, 0) M(NS, true, 1) M(NS, true, 2) M(NS, true, 3)
+#define GAR_HX_FOR_ALL(M)                                                                              \
+    GAR_HX_FOR_RB(M, 1) GAR_HX_FOR_RB(M, 2) GAR_HX_FOR_RB(M, 3) GAR_HX_FOR_RB(M, 4) GAR_HX_FOR_RB(M, 5) \
+    GAR_HX_FOR_RB(M, 6) GAR_HX_FOR_RB(M, 7) GAR_HX_FOR_RB(M, 8) GAR_HX_FOR_RB(M, 9) GAR_HX_FOR_RB(M, 10) \
+    M(2, false, 0) M(4, false, 0) M(6, false, 0) M(8, false, 0)
+#define GAR_HX_INST(NS, RB, V) template hipError_t hxLaunch<NS, RB, V>(const HxArgs&, int, size_t, int64_t, hipStream_t);
 
 }  // namespace gar
