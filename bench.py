@@ -252,7 +252,7 @@ def main():
             if launches else None,
         },
         "arith": ("f32 I/O; products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
-                  "(error below exact-f32 arithmetic: rms_vs_oracle)" if split else "exact f32 MFMA"),
+                  "(error at the level of exact-f32 arithmetic: rms_vs_oracle)" if split else "exact f32 MFMA"),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
