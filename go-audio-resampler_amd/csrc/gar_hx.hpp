@@ -401,25 +401,6 @@ __device__ __forceinline__ void firOne(const SrcDesc& src, const OutDesc& od, in
     if (lane == 0) outWrite<float>(od, o, c, s);
 }
 
-// Same, four outputs per wave (16 lanes each): lanes split the taps, 4-step
-// reduction inside the 16-lane group; o < 0 skips.
-__device__ __forceinline__ void firOne16(const SrcDesc& src, const OutDesc& od, int64_t o, int c, int P, int Q,
-                                         const int* rowOff, const int* rowLen, const float* rows, int rowMax, int l16) {
-    float s = 0.f;
-    int r = 0;
-    if (o >= 0) {
-        const int64_t a = o / P;
-        r = static_cast<int>(o - a * P);
-        const int64_t t = a * Q + rowOff[r];
-        const float* row = rows + static_cast<size_t>(r) * rowMax;
-        const int len = rowLen[r];
-        for (int k = l16; k < len; k += 16) s += row[k] * srcRead<float>(src, t + k, c);
-    }
-#pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-    if (o >= 0 && l16 == 0) outWrite<float>(od, o, c, s);
-}
-
 template <int NS, bool RB, bool SINGLE, int VST>
 __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -697,14 +678,12 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
             if (n > 0) {
                 const SrcDesc src = kload(&xc->src);
                 const OutDesc od = kload(&xc->od);
-                // four outputs per wave pass (one per 16-lane group)
-                for (int64_t i0 = (wg * NW + wt) * 4; i0 < n; i0 += static_cast<int64_t>(nwg) * NW * 4) {
-                    const int64_t idx = i0 + (lane >> 4);
+                for (int64_t idx = wg * NW + wt; idx < n; idx += static_cast<int64_t>(nwg) * NW) {
                     const bool first = idx < n0;
                     const int64_t k = first ? idx : idx - n0;
-                    const int64_t o = idx < n ? (first ? x.e0lo : x.e1lo) + k / x.C : -1;
-                    firOne16(src, od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, xc->rowOff, xc->rowLen, xc->rows,
-                             xc->rowMax, lane & 15);
+                    const int64_t o = (first ? x.e0lo : x.e1lo) + k / x.C;
+                    firOne(src, od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, xc->rowOff, xc->rowLen, xc->rows,
+                           xc->rowMax, lane);
                 }
             }
             const int64_t tn = xc->tn * x.C;  // history keep
