@@ -353,9 +353,8 @@ struct Ctx {
 };
 
 // launchBg bracketed by HIP events on the launch stream when profiling is on.
-hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C,
-                   TailCopy* tail = nullptr) {
-    if (!x.h->profile) return launchBg(p, src, od, C, x.s, tail);
+hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
+    if (!x.h->profile) return launchBg(p, src, od, C, x.s);
     hipEvent_t a, b;
     if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
         a = x.h->evPool.back().first;
@@ -366,7 +365,7 @@ hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const Ou
         HIPCHK(hipEventCreate(&b));
     }
     HIPCHK(hipEventRecord(a, x.s));
-    const hipError_t e = launchBg(p, src, od, C, x.s, tail);
+    const hipError_t e = launchBg(p, src, od, C, x.s);
     HIPCHK(hipEventRecord(b, x.s));
     x.h->events.push_back({tag, a, b});
     return e;
@@ -398,27 +397,6 @@ OutDesc mkOut(const OutView& o, int64_t o0, int64_t n) {
     d.o_lo = o0;
     d.o_hi = o0 + n;
     return d;
-}
-
-// The history-keep copy of hist_update, prepared for a FIR launch to absorb
-// (TailCopy); hist_commit then records the new history.
-TailCopy hist_tail(Ctx& x, Hist& hs, int64_t k0, int64_t k1) {
-    TailCopy t;
-    if (k1 < k0) k1 = k0;
-    const int C = x.g->C;
-    const int other = 1 - hs.cur;
-    hs.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(k1 - k0, 1)) * C * 4);
-    t.dst = static_cast<float*>(hs.buf[other].p);
-    t.t0 = k0;
-    t.n = k1 - k0;
-    return t;
-}
-void hist_commit(Hist& hs, int64_t k0, int64_t k1) {
-    if (k1 < k0) k1 = k0;
-    hs.cur = 1 - hs.cur;
-    hs.base = k0;
-    hs.len = k1 - k0;
-    hs.zero = false;
 }
 
 void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
@@ -504,18 +482,11 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t nout = cntPoly(c, d.poly, nu, quirk);
             if (!c.staged) {
                 // Fused: DFT x2 and polyphase composed into one MFMA FIR over x.
-                if (!quirk && x.launch && nout > 0 && !x.h->f64) {
-                    // the launch also keeps the history (no separate gather launch)
-                    TailCopy tc = hist_tail(x, dv.xh, c.u_base / 2, c.x_count);
-                    HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C, &tc));
-                    hist_commit(dv.xh, c.u_base / 2, c.x_count);
+                if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C));
+                if (quirk) {
+                    materialize(x, rt, c, dv, xsrc);
                 } else {
-                    if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C));
-                    if (quirk) {
-                        materialize(x, rt, c, dv, xsrc);
-                    } else {
-                        hist_update(x, dv.xh, xsrc, c.u_base / 2, c.x_count);
-                    }
+                    hist_update(x, dv.xh, xsrc, c.u_base / 2, c.x_count);
                 }
             } else {
                 // Staged: DFT (MFMA FIR) into u scratch, polyphase with live cubic interpolation.

@@ -60,7 +60,7 @@ int64_t ceilDiv(int64_t a, int64_t b) { return -floorDiv(-a, b); }
 
 }  // namespace
 
-hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, TailCopy* tail) {
+hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bits: 1 skip
     // staging after the first block, 2 skip the MFMA programs, 8 skip the fixup, 16 skip the loop,
@@ -163,12 +163,6 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     x.e0hi = x.a0 * Pc;
     x.e1lo = (a_lo + k1 * G) * Pc;
     x.e1hi = od.o_hi;
-    if (tail && tail->n > 0) {  // history keep: copied by the kernel's waves before the blocks
-        x.tdst = tail->dst;
-        x.tt0 = tail->t0;
-        x.tn = tail->n;
-        tail->n = 0;
-    }
 
     const size_t lds = ldsFor(G, parity);
     const int64_t blocks = std::min<int64_t>(x.nblocks, ncu);

@@ -72,8 +72,6 @@ struct HxArgs {
     int rowMax;
     const float* zero;
     int64_t e0lo, e0hi, e1lo, e1hi;  // launch edges [e0lo, e0hi) + [e1lo, e1hi): plain f32 FIR, spread over all waves
-    float* tdst;                     // history keep (TailCopy): source rows [tt0, tt0+tn) -> tdst[tn][C]
-    int64_t tt0, tn;
 };
 
 // ---- staging ----------------------------------------------------------------
@@ -444,6 +442,18 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
     // work) and publishing its quad maxima at the end.  Exponent sets rotate
     // over 4 (block k uses set k & 3): iteration it reads sets it, it+1, writes
     // it+2 and zeroes it+3 (last read in iteration it-1).
+    {  // launch edges (history seam, partial chunks): one output per wave at a time
+        const int64_t n0 = (x.e0hi - x.e0lo) * x.C, n = n0 + (x.e1hi - x.e1lo) * x.C;
+        for (int64_t idx = static_cast<int64_t>(blockIdx.x) * NW + wt; idx < n; idx += static_cast<int64_t>(gridDim.x) * NW) {
+            const bool first = idx < n0;
+            const int64_t k = first ? idx : idx - n0;
+            const int64_t o = (first ? x.e0lo : x.e1lo) + k / x.C;
+            const HxArgsK xc = hxCold();
+            const SrcDesc src = kload(&xc->src);
+            const OutDesc od = kload(&xc->od);
+            firOne(src, od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, xc->rowOff, xc->rowLen, xc->rows, xc->rowMax, lane);
+        }
+    }
     const HxItems items = hxItems(x.Ws, wt);
     f32x4 raw[kHxJ];
     if (threadIdx.x < 16) qeAll[threadIdx.x] = 0;
@@ -663,40 +673,6 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
         __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
         for (int j = 0; j < kHxJ; ++j) asm volatile("" : "+v"(raw[j]));
-    }
-    // Launch edges (history seam, partial chunks) and the history keep, after the
-    // blocks, on the workgroups with one block fewer (blockIdx >= nblocks % grid)
-    // when there are such: they finish a block early.
-    {
-        const int extra = x.nblocks % static_cast<int>(gridDim.x);
-        const int w0 = extra ? extra : 0;  // first slack workgroup
-        const int nwg = static_cast<int>(gridDim.x) - w0;
-        if (static_cast<int>(blockIdx.x) >= w0) {
-            const int64_t wg = blockIdx.x - w0;
-            const HxArgsK xc = hxCold();
-            const int64_t n0 = (x.e0hi - x.e0lo) * x.C, n = n0 + (x.e1hi - x.e1lo) * x.C;
-            if (n > 0) {
-                const SrcDesc src = kload(&xc->src);
-                const OutDesc od = kload(&xc->od);
-                for (int64_t idx = wg * NW + wt; idx < n; idx += static_cast<int64_t>(nwg) * NW) {
-                    const bool first = idx < n0;
-                    const int64_t k = first ? idx : idx - n0;
-                    const int64_t o = (first ? x.e0lo : x.e1lo) + k / x.C;
-                    firOne(src, od, o, static_cast<int>(k % x.C), x.Pc, x.Qc, xc->rowOff, xc->rowLen, xc->rows,
-                           xc->rowMax, lane);
-                }
-            }
-            const int64_t tn = xc->tn * x.C;  // history keep
-            if (tn > 0) {
-                const SrcDesc src = kload(&xc->src);
-                float* dst = xc->tdst;
-                const int64_t t0 = xc->tt0;
-                for (int64_t i = wg * blockDim.x + threadIdx.x; i < tn; i += static_cast<int64_t>(nwg) * blockDim.x) {
-                    const int64_t t = i / x.C;
-                    dst[i] = srcRead<float>(src, t0 + t, static_cast<int>(i - t * x.C));
-                }
-            }
-        }
     }
     if (!(x.dbg & 8)) {
         const HxArgs xc = kload(hxCold());

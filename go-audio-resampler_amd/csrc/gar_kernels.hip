@@ -26,19 +26,10 @@ hipError_t bgLaunchF32a(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                         size_t lds, int64_t blocks, hipStream_t st, bool globalB);
 
-hipError_t launchBgFir(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream);
-
-hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, TailCopy* tail) {
-    hipError_t e = (p.hx && !p.f64 && !src.in_f64) ? launchHx(*p.hx, src, od, C, stream, tail)
-                                                   : launchBgFir(p, src, od, C, stream);
-    if (e == hipSuccess && tail && tail->n > 0) e = launchGather(0, src, tail->dst, tail->t0, tail->n, C, stream);
-    return e;
-}
-
-hipError_t launchBgFir(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
+hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // f32 compute on the split-f16 kernel; f64 input (float64 API on a float32 engine) stays on exact f32
-
+    if (p.hx && !p.f64 && !src.in_f64) return launchHx(*p.hx, src, od, C, stream);
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;

@@ -68,16 +68,8 @@ struct PolyDev {
 };
 
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
-// History keep folded into the FIR launch: rows [t0, t0+n) of the launch's source (all channels, f32)
-// copied to dst [n][C].  launchBg does it with gather_kernel unless the launch absorbed it (n set to 0).
-struct TailCopy {
-    float* dst = nullptr;
-    int64_t t0 = 0, n = 0;
-};
-hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
-                    TailCopy* tail = nullptr);
-hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
-                    TailCopy* tail);
+hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
                       hipStream_t stream);
 // dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.
