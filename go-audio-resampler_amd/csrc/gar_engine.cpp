@@ -886,6 +886,33 @@ gar_status newCommon(gar_config* cfg, int32_t nstreams, gar_resampler** out) {
     });
 }
 
+// engine.NewResampler[F] behind NewEngine / NewEngineFloat32 / the engine seam
+// (convenience.go:125-135, :329-336; internal/engine/resampler.go:51-179).
+gar_status newEngineCommon(double in_rate, double out_rate, Quality q, int32_t dtype, bool dry, gar_resampler** out) {
+    if (!out) return guard(GAR_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    if (dtype != GAR_F64 && dtype != GAR_F32 && dtype != GAR_F32_EXACT) return guard(GAR_ERR_INVALID_ARGUMENT, "unknown dtype");
+    if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
+    auto h = std::make_unique<gar_resampler>();
+    h->newPath = false;
+    h->channels = 1;
+    h->dry = dry;
+    h->f64 = dtype == GAR_F64;
+    h->hx = dtype == GAR_F32 && hxEnabled();
+    h->engineF32Io = dtype != GAR_F64;
+    h->ratio = out_rate / in_rate;
+    return wrap([&]() -> gar_status {
+        gar_status st = initDevice(h.get());
+        if (st != GAR_OK) return st;
+        st = addStage(h.get(), in_rate, out_rate, q);
+        if (st != GAR_OK) return st;
+        h->ratio = h->stages[0]->d.ratio;
+        h->groups.push_back(freshGroup(h.get(), 0, 1));
+        *out = h.release();
+        return GAR_OK;
+    });
+}
+
 int64_t estimate(const Handle* h, int64_t n) {
     return static_cast<int64_t>(static_cast<double>(n) * h->ratio) + 64;
 }
@@ -963,46 +990,21 @@ gar_status gar_new_batch(gar_config* cfg, int32_t n_streams, gar_resampler** out
 }
 
 gar_status gar_new_engine(double in_rate, double out_rate, int32_t preset, int32_t dtype, gar_resampler** out) {
-    if (!out) return guard(GAR_ERR_INVALID_ARGUMENT, "out is NULL");
-    *out = nullptr;
-    auto h = std::make_unique<gar_resampler>();
-    h->newPath = false;
-    h->channels = 1;
-    h->f64 = dtype != GAR_F32;
-    h->hx = dtype == GAR_F32 && hxEnabled();
-    h->engineF32Io = dtype == GAR_F32;
-    if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
-    h->ratio = out_rate / in_rate;
-    return wrap([&]() -> gar_status {
-        gar_status st = initDevice(h.get());
-        if (st != GAR_OK) return st;
-        st = addStage(h.get(), in_rate, out_rate, presetToEngineQuality(preset));
-        if (st != GAR_OK) return st;
-        h->ratio = h->stages[0]->d.ratio;
-        h->groups.push_back(freshGroup(h.get(), 0, 1));
-        *out = h.release();
-        return GAR_OK;
-    });
+    return newEngineCommon(in_rate, out_rate, presetToEngineQuality(preset), dtype, false, out);
+}
+
+gar_status gar_new_engine_quality(double in_rate, double out_rate, int32_t engine_quality, int32_t dtype,
+                                  gar_resampler** out) {
+    if (engine_quality < GAR_ENGINE_QUICK || engine_quality > GAR_ENGINE_32BIT) {
+        if (out) *out = nullptr;
+        return guard(GAR_ERR_INVALID_CONFIG, "unknown engine quality");
+    }
+    return newEngineCommon(in_rate, out_rate, static_cast<Quality>(engine_quality), dtype, false, out);
 }
 
 gar_status gar_new_engine_dry(double in_rate, double out_rate, int32_t preset, int32_t dtype, gar_resampler** out) {
     // Host-only engine (used by CPU tests of the stream-length state machine).
-    if (!out) return GAR_ERR_INVALID_ARGUMENT;
-    *out = nullptr;
-    auto h = std::make_unique<gar_resampler>();
-    h->newPath = false;
-    h->dry = true;
-    h->f64 = dtype != GAR_F32;
-    h->hx = dtype == GAR_F32 && hxEnabled();
-    if (!(in_rate > 0) || !(out_rate > 0)) return guard(GAR_ERR_INVALID_CONFIG, "sample rates must be positive");
-    return wrap([&]() -> gar_status {
-        gar_status st = addStage(h.get(), in_rate, out_rate, presetToEngineQuality(preset));
-        if (st != GAR_OK) return st;
-        h->ratio = h->stages[0]->d.ratio;
-        h->groups.push_back(freshGroup(h.get(), 0, 1));
-        *out = h.release();
-        return GAR_OK;
-    });
+    return newEngineCommon(in_rate, out_rate, presetToEngineQuality(preset), dtype, true, out);
 }
 
 void gar_free(gar_resampler* r) {

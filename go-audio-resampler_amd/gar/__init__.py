@@ -83,7 +83,7 @@ class EngineGeometry(C.Structure):
 
 
 EXPORTED = [
-    "gar_config_validate", "gar_preset_spec", "gar_new", "gar_new_batch", "gar_new_engine", "gar_new_engine_dry", "gar_free",
+    "gar_config_validate", "gar_preset_spec", "gar_new", "gar_new_batch", "gar_new_engine", "gar_new_engine_quality", "gar_new_engine_dry", "gar_free",
     "gar_estimate_output", "gar_output_size", "gar_flush_size", "gar_process_f64", "gar_process_f32",
     "gar_process_into_f64", "gar_process_into_f32", "gar_process_multi_f64", "gar_flush_f64", "gar_flush_f32",
     "gar_flush_multi_f64", "gar_process_device", "gar_flush_device", "gar_device_output_size",
@@ -118,6 +118,7 @@ def lib():
         "gar_new": (i32, [C.POINTER(_Config), C.POINTER(vp)]),
         "gar_new_batch": (i32, [C.POINTER(_Config), i32, C.POINTER(vp)]),
         "gar_new_engine": (i32, [d, d, i32, i32, C.POINTER(vp)]),
+        "gar_new_engine_quality": (i32, [d, d, i32, i32, C.POINTER(vp)]),
         "gar_new_engine_dry": (i32, [d, d, i32, i32, C.POINTER(vp)]),
         "gar_free": (None, [vp]),
         "gar_estimate_output": (i64, [vp, i64]),
@@ -358,6 +359,15 @@ def NewEngineFloat32(inputRate, outputRate, quality):
     h = C.c_void_p(0)
     _check(lib().gar_new_engine(float(inputRate), float(outputRate), quality, F32, C.byref(h)))
     return Resampler(h.value, f32_io=True)
+
+
+def EngineNewResampler(inputRate, outputRate, quality, dtype=F64):
+    """engine.NewResampler[F](inputRate, outputRate, quality) with an engine.Quality
+    (internal/engine/resampler.go:51-179; the seam cmd/resample-wav/helpers.go:77-97
+    drives).  dtype F64 = Resampler[float64]; F32 / F32_EXACT = Resampler[float32]."""
+    h = C.c_void_p(0)
+    _check(lib().gar_new_engine_quality(float(inputRate), float(outputRate), int(quality), int(dtype), C.byref(h)))
+    return Resampler(h.value, f32_io=dtype != F64)
 
 
 def NewEngineDry(inputRate, outputRate, quality, dtype=F64):

@@ -105,6 +105,13 @@ gar_status gar_new_batch(gar_config *cfg, int32_t n_streams, gar_resampler **out
 gar_status gar_new_engine(double input_rate, double output_rate, int32_t preset, int32_t dtype,
                           gar_resampler **out);
 void gar_free(gar_resampler *r);
+/* engine.NewResampler[F](in, out, quality) (internal/engine/resampler.go:51-179)
+ * with an engine.Quality (GAR_ENGINE_*) -- the engine seam cmd/resample-wav
+ * drives directly (cmd/resample-wav/helpers.go:77-97) and the reference's
+ * engine tests use.  dtype GAR_F64 = Resampler[float64]; GAR_F32 /
+ * GAR_F32_EXACT = Resampler[float32] (float32 I/O). */
+gar_status gar_new_engine_quality(double input_rate, double output_rate, int32_t engine_quality, int32_t dtype,
+                                  gar_resampler **out);
 /* Host-only NewEngine (no GPU work; process calls report exact lengths only).
  * Used to test the stream-length state machine on machines without a GPU. */
 gar_status gar_new_engine_dry(double input_rate, double output_rate, int32_t preset, int32_t dtype,
