@@ -115,6 +115,11 @@ template <> struct Acc<double> {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Sets a kernel's 160 KiB dynamic-LDS attribute once per (device, kernel):
+// the attribute is per device, and handles on several devices may launch
+// from several host threads (gar_kernels.hip).
+void setMaxLdsOnce(const void* fn);
+
 // Input element kk of column `col`'s window (column = channel c, chunk of G
 // macro periods).  Fast path when the whole window lies in one buffer.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -419,18 +424,10 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
 template <class TC, int NS>
 static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                              size_t lds, int64_t blocks, hipStream_t st, bool globalB) {
-    static bool attrSet = false;
-    if (!attrSet) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, true>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, false>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attrSet = true;
-    }
+    setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, true>));
+    setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, false>));
+    setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, true>));
+    setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, false>));
     if (threads > bgMaxThreads(sizeof(TC) == 8, NS)) return hipErrorInvalidConfiguration;
     const dim3 gd(static_cast<unsigned>(blocks)), bd(threads);
     const bool single = g.kch == 1;

@@ -86,27 +86,32 @@ struct StageRT {
     // split-f16 variants (f32 compute), referenced from the BgDev's .hx
     struct HxRT {
         HxPlan plan;
-        DevBuf A, T, rows, roff, rlen, fix;
+        DevBuf A, T, rows, rowInfo, banks, banks2, fix;
         HxDev d{};
     } fusedH, dftH, decimH;
 
     int tc() const { return f64 ? 8 : 4; }
 };
 
-// Builds + uploads the split-f16 plan of `f` and points bg.hx at it.
-bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry) {
+// Builds + uploads the split-f16 plan of `f` and points bg.hx at it; `ed` (the
+// engine design) supplies the two stages of a composite FIR for the exact
+// fallback of non-finite windows.
+bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry, const EngineDesign& ed) {
     if (!buildHxPlan(f, h.plan)) return false;
     HxDev& d = h.d;
     const HxPlan& p = h.plan;
     // two double-buffered hi/lo images of one macro period + one partial-slot buffer must fit LDS;
     // longer filters (e.g. the 1223-tap decimator) stay on the exact-f32 kernel
-    const size_t ws1 = (static_cast<size_t>(p.Kread) + 7) / 8 * 8;
+    const size_t ws1 = (static_cast<size_t>(p.Kread) + 63) / 64 * 64;
     if (ws1 > static_cast<size_t>(kHxMaxRows)) return false;
-    if (4 * ws1 * 32 + static_cast<size_t>(p.nslots) * 256 * 4 + 128 > 160 * 1024) return false;
+    if (hxLdsBytes(static_cast<int>(ws1), p.nslots, 0) > 160 * 1024) return false;
     d = HxDev{};
     d.Pc = p.Pc; d.Qc = p.Qc; d.Kc = p.Kc; d.Kread = p.Kread; d.NS = p.NS; d.nrb = p.nrb;
     d.nw = p.nw; d.kch = p.kch; d.nred = static_cast<int>(p.reds.size()); d.nslots = p.nslots;
     d.ea = p.ea; d.rowMax = p.rowMax; d.rb = p.rbMode ? 1 : 0;
+    d.twoStage = p.twoStage ? 1 : 0;
+    d.T1 = ed.dft.taps;
+    d.T2 = ed.poly.taps;
     if (!dry) {
         h.A.upload(p.A);
         std::vector<int> t = p.progTable();
@@ -115,18 +120,28 @@ bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry) {
         t.insert(t.end(), rt.begin(), rt.end());
         h.T.upload(t);
         h.rows.upload(p.rows);
-        h.roff.upload(p.rowOff);
-        h.rlen.upload(p.rowLen);
+        std::vector<int> ri = p.rowOff;  // [rowOff | rowLen | rowPh | rowPar]
+        ri.insert(ri.end(), p.rowLen.begin(), p.rowLen.end());
+        ri.insert(ri.end(), p.rowPh.begin(), p.rowPh.end());
+        ri.insert(ri.end(), p.rowPar.begin(), p.rowPar.end());
+        h.rowInfo.upload(ri);
         d.A = h.A.p;
         d.progs = static_cast<const int*>(h.T.p);
         d.reds = static_cast<const int*>(h.T.p) + redOff;
-        d.rows = static_cast<const float*>(h.rows.p);
-        d.rowOff = static_cast<const int*>(h.roff.p);
-        d.rowLen = static_cast<const int*>(h.rlen.p);
-        d.fixCap = 4096;
-        h.fix.upload(std::vector<int>(2 + d.fixCap + 64 + 256, 0));  // list, 64 zero words, 1 KiB store sink
+        d.rows = static_cast<const double*>(h.rows.p);
+        d.rowOff = static_cast<const int*>(h.rowInfo.p);
+        d.rowLen = d.rowOff + p.Pc;
+        d.rowPh = d.rowOff + 2 * p.Pc;
+        d.rowPar = d.rowOff + 3 * p.Pc;
+        d.fixCap = 1 << 16;
+        h.fix.upload(std::vector<int>(1 + d.fixCap, 0));
         d.fix = static_cast<int*>(h.fix.p);
-        d.zero = reinterpret_cast<const float*>(d.fix + 2 + d.fixCap);  // 64 zero words past the list
+        if (p.twoStage) {
+            h.banks.upload(ed.poly.a);
+            h.banks2.upload(ed.dft.c);
+            d.polyA = static_cast<const double*>(h.banks.p);
+            d.dftC = static_cast<const double*>(h.banks2.p);
+        }
     }
     bg.hx = &h.d;
     return true;
@@ -169,18 +184,18 @@ bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
     if (d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) {
         if (!buildBgPlan(firFromDft(d.dft), f64, s.dftP)) { err = "DFT plan"; return false; }
         s.dftD = uploadPlan(s.dftP, s.dftA, s.dftT, dry);
-        if (hx) attachHx(firFromDft(d.dft), s.dftH, s.dftD, dry);
+        if (hx) attachHx(firFromDft(d.dft), s.dftH, s.dftD, dry, d);
     }
     if (d.kind == EngineKind::Decim) {
         if (!buildBgPlan(firFromDecim(d.decim), f64, s.decimP)) { err = "decimator plan"; return false; }
         s.decimD = uploadPlan(s.decimP, s.decimA, s.decimT, dry);
-        if (hx) attachHx(firFromDecim(d.decim), s.decimH, s.decimD, dry);
+        if (hx) attachHx(firFromDecim(d.decim), s.decimH, s.decimD, dry, d);
     }
     if (d.kind == EngineKind::DftPoly) {
         if (firComposite(d.dft, d.poly, s.compositeFir) && buildBgPlan(s.compositeFir, f64, s.fusedP)) {
             s.fused = true;
             s.fusedD = uploadPlan(s.fusedP, s.fusedA, s.fusedT, dry);
-            if (hx) attachHx(s.compositeFir, s.fusedH, s.fusedD, dry);
+            if (hx) attachHx(s.compositeFir, s.fusedH, s.fusedD, dry, d);
         }
         PolyDev& p = s.polyD;
         p.f64 = f64 ? 1 : 0;

@@ -15,11 +15,24 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <set>
+#include <utility>
 
 #include "gar_bg.hpp"
 #include "gar_kernels.hpp"
 
 namespace gar {
+
+void setMaxLdsOnce(const void* fn) {
+    static std::mutex mu;
+    static std::set<std::pair<int, const void*>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!done.insert({dev, fn}).second) return;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
 
 hipError_t bgLaunchF32a(int NS, const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                         size_t lds, int64_t blocks, hipStream_t st, bool globalB);
@@ -28,8 +41,8 @@ hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
-    // f32 compute on the split-f16 kernel; f64 input (float64 API on a float32 engine) stays on exact f32
-    if (p.hx && !p.f64 && !src.in_f64) return launchHx(*p.hx, src, od, C, stream);
+    // f32 compute on the split-f16 kernel (every output of the launch, any input dtype)
+    if (p.hx && !p.f64) return launchHx(*p.hx, src, od, C, stream);
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;

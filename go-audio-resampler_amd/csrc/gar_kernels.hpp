@@ -47,15 +47,21 @@ struct HxDev {
     int Pc, Qc, Kc, Kread, NS, nrb;
     int nw, kch, nred, nslots, ea, rowMax;
     int rb;              // row-block mode (HxPlan::rbMode)
-    int fixCap;          // capacity of the non-finite block list
-    int* fix;            // [2 + fixCap]: count, finished workgroups, block ids (zero between launches)
-    const float* zero;   // a zero float (LDS-DMA source of flush zeros / out-of-range rows)
     const void* A;       // [nw][kch*NS][2][64][8] f16
     const int* progs;    // [nw][kBgProgInts] (HxPlan::progTable)
     const int* reds;     // [nred][kBgRedInts]
-    const float* rows;   // non-finite fallback rows [Pc][rowMax]
+    // exact fallback of outputs whose windows hold |x| >= 16 / Inf / NaN
+    const double* rows;  // [Pc][rowMax] FIR rows (f64)
     const int* rowOff;   // [Pc]
     const int* rowLen;   // [Pc]
+    int twoStage;        // rows are DFT x2 (*) polyphase composites (HxPlan::twoStage)
+    int T1, T2;          // DFT taps per phase, polyphase taps per phase
+    const int* rowPh;    // [Pc] polyphase phase of each composite row
+    const int* rowPar;   // [Pc] DFT output parity of each composite row
+    const double* polyA; // [L][T2]
+    const double* dftC;  // [2][T1]
+    int* fix;            // [1 + fixCap]: interior blocks holding loud elements (count first)
+    int fixCap;
 };
 
 // General polyphase stage with live cubic coefficient interpolation

@@ -53,6 +53,7 @@ bool firComposite(const DftBank& d, const PolyBank& p, FirPeriodic& f) {
     const int64_t L = p.L;
     const int64_t g2 = std::gcd<int64_t>(S, 2 * L);
     f = FirPeriodic();
+    f.composite = true;
     f.P = static_cast<int>(2 * L / g2);
     f.Q = static_cast<int>(S / g2);
     const int T1 = d.taps, T2 = p.taps;
@@ -62,6 +63,8 @@ bool firComposite(const DftBank& d, const PolyBank& p, FirPeriodic& f) {
         const int ph = static_cast<int>(full % L);
         const int par = static_cast<int>(dd & 1);
         f.off.push_back(dd >> 1);
+        f.ph.push_back(ph);
+        f.par.push_back(par);
         const int ng = ((par + T2 - 1) >> 1) + T1;
         std::vector<double> row(ng, 0.0);
         const double* a = p.a.data() + static_cast<long>(ph) * T2;
@@ -422,16 +425,23 @@ bool buildHxPlan(const FirPeriodic& f, HxPlan& plan) {
 
     plan.rowMax = 0;
     for (const auto& r : f.rows) plan.rowMax = std::max(plan.rowMax, static_cast<int>(r.size()));
-    plan.rows.assign(static_cast<size_t>(plan.Pc) * plan.rowMax, 0.f);
+    plan.rows.assign(static_cast<size_t>(plan.Pc) * plan.rowMax, 0.0);
     plan.rowOff.assign(plan.Pc, 0);
     plan.rowLen.assign(plan.Pc, 0);
+    plan.twoStage = f.composite;
+    plan.rowPh.assign(plan.Pc, 0);
+    plan.rowPar.assign(plan.Pc, 0);
     for (int r = 0; r < plan.Pc; ++r) {
         int64_t off;
         const std::vector<double>* row;
         macroRow(f, r, off, row);
         plan.rowOff[r] = static_cast<int>(off);
         plan.rowLen[r] = static_cast<int>(row->size());
-        for (size_t k = 0; k < row->size(); ++k) plan.rows[static_cast<size_t>(r) * plan.rowMax + k] = static_cast<float>((*row)[k]);
+        for (size_t k = 0; k < row->size(); ++k) plan.rows[static_cast<size_t>(r) * plan.rowMax + k] = (*row)[k];
+        if (f.composite) {
+            plan.rowPh[r] = f.ph[r % f.P];
+            plan.rowPar[r] = f.par[r % f.P];
+        }
     }
 
     double useful = 0;

@@ -23,6 +23,10 @@ struct FirPeriodic {
     int P = 0, Q = 0;                 // outputs / inputs per period
     std::vector<int64_t> off;         // [P] input offset of output r within the period
     std::vector<std::vector<double>> rows;  // [P] coefficient row (multiplies v[s+k])
+    // composite rows only (firComposite): row r = polyphase phase ph[r] of the DFT
+    // output stream starting at parity par[r]
+    bool composite = false;
+    std::vector<int> ph, par;
 };
 
 FirPeriodic firFromDft(const DftBank& d);
@@ -97,6 +101,7 @@ constexpr int kHxRbMaxNS = 10;     // row-block mode register budget (168 VGPRs)
 constexpr int kHxMaxRows = 1024;   // window rows per block (4*1024 staged items: 7 per lane at 10 waves)
 constexpr int kHxMinWaves = 10;    // waves per workgroup (waves past the programs only stage)
 constexpr int kHxMaxWaves = 10;    // __launch_bounds__ (3 waves per SIMD: 168 VGPRs)
+constexpr int kHxFixWgs = 32;      // extra workgroups of the edge launch that drain the fix list
 inline int hxPermK(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
 struct HxPlan {
@@ -110,9 +115,11 @@ struct HxPlan {
     std::vector<BgProg> progs;        // [nw]; BgSeg::k0 = first input row of the segment
     std::vector<BgRed> reds;
     std::vector<uint16_t> A;          // [nw][kch*NS][2 (hi, lo)][64 lanes][8] f16 bits
-    int rowMax = 0;                   // non-finite fallback: f32 rows [Pc][rowMax], offsets, lengths
-    std::vector<float> rows;
+    int rowMax = 0;                   // exact fallback (loud windows): f64 rows [Pc][rowMax], offsets, lengths
+    std::vector<double> rows;
     std::vector<int> rowOff, rowLen;
+    bool twoStage = false;            // composite rows: per-row polyphase phase / DFT parity
+    std::vector<int> rowPh, rowPar;
     double usefulMacsPerOutput = 0;
     double mfmaMacsPerOutput = 0;     // executed MACs (one of the three products) per output
     std::vector<int> progTable() const;  // [nw][kBgProgInts]
@@ -120,5 +127,12 @@ struct HxPlan {
 };
 
 bool buildHxPlan(const FirPeriodic& f, HxPlan& plan);
+
+// LDS bytes of one hx launch with Ws window rows per column: two hi/lo image
+// buffers, partial slots, the loud-element masks [2][16][Ws/32] + flags.
+inline size_t hxLdsBytes(int Ws, int nslots, int parity) {
+    return 8 * (16 * static_cast<size_t>(Ws) + 64) + static_cast<size_t>(parity ? 2 : 1) * nslots * 256 * 4 +
+           (2 * 16 * static_cast<size_t>(Ws / 32) + 2) * 4 + 16;
+}
 
 }  // namespace gar

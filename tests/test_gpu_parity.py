@@ -172,26 +172,30 @@ def test_process_into_equals_process(gar, cuda):  # processinto_test.go:36-104
         np.testing.assert_array_equal(buf[:n], want)
 
 
-@pytest.mark.parametrize("dtype", ["F32_EXACT", "F64"])
+@pytest.mark.parametrize("dtype", ["F32", "F32_EXACT", "F64"])
 def test_chunking_is_bit_identical(gar, cuda, dtype):  # processinto_test.go:258-308
+    """Any chunking == one shot, bit for bit, on every compute path (GAR_F32 included:
+    its split scale is a constant, so an output depends only on its own window)."""
     dt = getattr(gar, dtype)
     x = signal(60000, 2, 44100)
     one = dev_run(gar, cuda, 44100, 48000, x, gar.QualityHigh, dt)
-    for size in (4800, 4096, 333):
-        np.testing.assert_array_equal(dev_run(gar, cuda, 44100, 48000, x, gar.QualityHigh, dt,
-                                              chunk_sizes(60000, size)), one)
+    for size in (4800, 4096, 333, 1):
+        n = 60000 if size > 1 else 3000
+        ref = one if size > 1 else dev_run(gar, cuda, 44100, 48000, x[:n], gar.QualityHigh, dt)
+        np.testing.assert_array_equal(dev_run(gar, cuda, 44100, 48000, x[:n], gar.QualityHigh, dt,
+                                              chunk_sizes(n, size)), ref)
 
 
-def test_chunking_f32_split_within_tolerance(gar, cuda):  # processinto_test.go:258-308
-    """GAR_F32 (split-f16 products): per-block power-of-two scaling and exact-f32 call
-    edges make chunked output agree with one shot to the split's ~2^-22, not bit for bit."""
-    x = signal(60000, 2, 44100)
-    one = dev_run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32).astype(np.float64)
-    for size in (4800, 4096, 333):
-        got = dev_run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32, chunk_sizes(60000, size))
-        assert got.shape == one.shape
-        assert np.max(np.abs(got - one)) <= 2e-6
-        assert np.sqrt(np.mean((got - one) ** 2)) <= 2e-7
+@pytest.mark.parametrize("case", [(48000, 44100, 5, "QualityVeryHigh"), (96000, 44100, 3, "QualityVeryHigh"),
+                                  (22050, 44100, 1, "QualityHigh"), (44100, 96000, 4, "QualityLow")])
+def test_chunking_is_bit_identical_f32_pipelines(gar, cuda, case):
+    """GAR_F32 chunk invariance across the other engine kinds and multi-stage pipelines."""
+    ir, orr, ch, q = case
+    x = signal(30011, ch, ir, seed=5)
+    one = dev_run(gar, cuda, ir, orr, x, getattr(gar, q), gar.F32)
+    for size in (4096, 777):
+        np.testing.assert_array_equal(dev_run(gar, cuda, ir, orr, x, getattr(gar, q), gar.F32,
+                                              chunk_sizes(30011, size)), one)
 
 
 def test_stereo_equals_two_monos(gar, cuda):  # convenience_stereo_test.go:40-106
