@@ -341,6 +341,15 @@ struct gar_resampler {
     int device = 0;
     bool engineF32Io = false;
     hipStream_t stream = nullptr;
+    // cross-stream ordering: every call's work is recorded on orderEv; a call on another
+    // stream waits for it first, so one handle's launches never overlap (they share
+    // histories, scratch and the fix lists)
+    hipEvent_t orderEv = nullptr;
+    hipStream_t lastStream = nullptr;
+    bool orderValid = false;
+    // a HIP failure mid-call may leave counters advanced past the histories: refuse
+    // further work until Reset (ADVICE: no silent wrong output)
+    bool poisoned = false;
     gar_config cfg{};
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
@@ -784,6 +793,21 @@ gar_status guard(gar_status s, const char* msg) {
     return s;
 }
 
+// Makes the handle's device current for one call and restores the caller's.
+struct DeviceGuard {
+    int prev = -1;
+    bool set = false;
+    explicit DeviceGuard(int dev) {
+        if (dev < 0) return;
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev && hipSetDevice(dev) == hipSuccess) set = true;
+    }
+    ~DeviceGuard() {
+        if (set) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 template <class F>
 gar_status wrap(F&& f) {
     try {
@@ -795,6 +819,26 @@ gar_status wrap(F&& f) {
         g_err = "out of host memory";
         return GAR_ERR_INTERNAL;
     }
+}
+
+// One ABI call that touches the device: handle's device current, ordered after
+// the handle's previous call (any stream), recorded for the next; a device
+// error poisons the handle until Reset.
+template <class F>
+gar_status callOn(Handle* h, hipStream_t s, F&& f) {
+    if (h->poisoned) return guard(GAR_ERR_DEVICE, "handle unusable after an earlier device error; call Reset");
+    if (h->dry) return wrap(f);
+    DeviceGuard dg(h->device);
+    const gar_status st = wrap([&]() -> gar_status {
+        if (h->orderValid && h->lastStream != s) HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
+        const gar_status r = f();
+        HIPCHK(hipEventRecord(h->orderEv, s));
+        h->lastStream = s;
+        h->orderValid = true;
+        return r;
+    });
+    if (st == GAR_ERR_DEVICE) h->poisoned = true;
+    return st;
 }
 
 // Precision carried by a preset (resample.go:217-267).
@@ -849,6 +893,7 @@ gar_status initDevice(Handle* h) {
     }
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&h->orderEv, hipEventDisableTiming));
     return GAR_OK;
 }
 
@@ -880,6 +925,7 @@ gar_status newCommon(gar_config* cfg, int32_t nstreams, gar_resampler** out) {
     h->hx = cfg->compute_dtype == GAR_F32 && hxEnabled();
     h->dry = cfg->dry_run != 0;
     h->device = cfg->device;
+    DeviceGuard dg(h->dry ? -1 : cfg->device);
     return wrap([&]() -> gar_status {
         gar_status st = initDevice(h.get());
         if (st != GAR_OK) return st;
@@ -916,6 +962,7 @@ gar_status newEngineCommon(double in_rate, double out_rate, Quality q, int32_t d
     h->hx = dtype == GAR_F32 && hxEnabled();
     h->engineF32Io = dtype != GAR_F64;
     h->ratio = out_rate / in_rate;
+    DeviceGuard dg(dry ? -1 : 0);
     return wrap([&]() -> gar_status {
         gar_status st = initDevice(h.get());
         if (st != GAR_OK) return st;
@@ -956,7 +1003,7 @@ gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t c
     if (!flush && n < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
     if (!flush && intoSemantics && cap < estimate(h, n)) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
     const int f64 = sizeof(T) == 8 ? 1 : 0;
-    return wrap([&]() -> gar_status {
+    return callOn(h, h->stream, [&]() -> gar_status {
         isolate(h, ch);
         Group* g = groupOf(h, ch);
         std::vector<int64_t> sizes;
@@ -1024,8 +1071,11 @@ gar_status gar_new_engine_dry(double in_rate, double out_rate, int32_t preset, i
 
 void gar_free(gar_resampler* r) {
     if (!r) return;
+    DeviceGuard dg(r->dry ? -1 : r->device);
     try {
         if (r->stream) (void)hipStreamSynchronize(r->stream);
+        if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
+        if (r->orderEv) (void)hipEventDestroy(r->orderEv);
         for (auto& ev : r->events) {
             (void)hipEventDestroy(ev.a);
             (void)hipEventDestroy(ev.b);
@@ -1088,7 +1138,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
         g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(nch);
         return GAR_ERR_CHANNEL_MISMATCH;
     }
-    return wrap([&]() -> gar_status {
+    return callOn(r, r->stream, [&]() -> gar_status {
         gar_resampler* h = r;
         // exact sizes first: no state changes on BUFFER_TOO_SMALL
         for (auto& g : h->groups) {
@@ -1135,7 +1185,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
 gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch, int64_t cap, int64_t* n_out) {
     if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
     if (nch != r->channels) return guard(GAR_ERR_CHANNEL_MISMATCH, "channel count mismatch");
-    return wrap([&]() -> gar_status {
+    return callOn(r, r->stream, [&]() -> gar_status {
         gar_resampler* h = r;
         for (auto& g : h->groups) {
             std::vector<int64_t> s;
@@ -1180,12 +1230,18 @@ int64_t gar_device_flush_size(const gar_resampler* r) {
 }
 
 gar_status gar_process_device(gar_resampler* r, const void* in, int32_t in_dtype, int64_t in_fs, int64_t in_cs,
-                              int64_t frames, void* out, int32_t out_dtype, int64_t out_fs, int64_t out_cs,
-                              int64_t out_cap, int64_t* out_frames, void* stream) {
+                              int64_t frames, int32_t channels, void* out, int32_t out_dtype, int64_t out_fs,
+                              int64_t out_cs, int64_t out_cap, int64_t* out_frames, void* stream) {
     if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
-    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep (per-channel calls were made)");
     if (out_frames) *out_frames = 0;
-    return wrap([&]() -> gar_status {
+    if (channels != r->channels) {
+        g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(channels);
+        return GAR_ERR_CHANNEL_MISMATCH;
+    }
+    if (frames < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
+    if (frames > 0 && !in) return guard(GAR_ERR_INVALID_ARGUMENT, "input is NULL");
+    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep (per-channel calls were made)");
+    return callOn(r, static_cast<hipStream_t>(stream), [&]() -> gar_status {
         InView iv;
         iv.p = in;
         iv.f64 = in_dtype == GAR_F64 ? 1 : 0;
@@ -1205,12 +1261,16 @@ gar_status gar_process_device(gar_resampler* r, const void* in, int32_t in_dtype
     });
 }
 
-gar_status gar_flush_device(gar_resampler* r, void* out, int32_t out_dtype, int64_t out_fs, int64_t out_cs,
-                            int64_t out_cap, int64_t* out_frames, void* stream) {
+gar_status gar_flush_device(gar_resampler* r, int32_t channels, void* out, int32_t out_dtype, int64_t out_fs,
+                            int64_t out_cs, int64_t out_cap, int64_t* out_frames, void* stream) {
     if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
-    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep");
     if (out_frames) *out_frames = 0;
-    return wrap([&]() -> gar_status {
+    if (channels != r->channels) {
+        g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(channels);
+        return GAR_ERR_CHANNEL_MISMATCH;
+    }
+    if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep");
+    return callOn(r, static_cast<hipStream_t>(stream), [&]() -> gar_status {
         OutView ov;
         ov.p = out;
         ov.f64 = out_dtype == GAR_F64 ? 1 : 0;
@@ -1226,7 +1286,17 @@ gar_status gar_flush_device(gar_resampler* r, void* out, int32_t out_dtype, int6
 
 void gar_reset(gar_resampler* r) {
     if (!r) return;
+    DeviceGuard dg(r->dry ? -1 : r->device);
     try {
+        if (r->poisoned) {  // recover: drain the handle's streams, fresh state
+            if (r->stream) (void)hipStreamSynchronize(r->stream);
+            if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
+            (void)hipGetLastError();
+            r->groups.clear();
+            r->groups.push_back(freshGroup(r, 0, r->channels));
+            r->poisoned = false;
+            return;
+        }
         // one group over every channel: reset in place, keeping its device buffers
         // (stream order covers kernels still reading them; no allocation, no sync)
         if (r->groups.size() == 1 && r->groups[0].c0 == 0 && r->groups[0].C == r->channels) {
@@ -1242,6 +1312,7 @@ void gar_reset(gar_resampler* r) {
             return;
         }
         if (r->stream) (void)hipStreamSynchronize(r->stream);
+        if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
         r->groups.clear();
         r->groups.push_back(freshGroup(r, 0, r->channels));
     } catch (...) {
@@ -1306,6 +1377,7 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
 
 gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t* launches) {
     if (!r || kind < 0 || kind > 3) return GAR_ERR_INVALID_ARGUMENT;
+    DeviceGuard dg(r->dry ? -1 : r->device);
     return wrap([&]() -> gar_status {
         for (auto& ev : r->events) {
             HIPCHK(hipEventSynchronize(ev.b));

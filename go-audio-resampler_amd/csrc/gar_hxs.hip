@@ -1,0 +1,186 @@
+// gar_hxs.hip -- launch geometry of the streaming split-f16 kernel (gar_hxs.hpp)
+// for row-block plans.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "gar_hxs.hpp"
+
+namespace gar {
+
+// instantiations live in gar_hxs_i1.hip / gar_hxs_i2.hip (compiled in parallel)
+#define GAR_HXS_EXT(NS, V) extern template hipError_t hxsLaunch<NS, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+GAR_HXS_FOR_ALL(GAR_HXS_EXT)
+#undef GAR_HXS_EXT
+
+namespace {
+// development: GAR_HXS_PROF=1 sums per-phase s_memtime cycles of every launch and prints them at exit
+unsigned long long* profBuf() {
+    static unsigned long long* p = nullptr;
+    static bool init = false;
+    if (!init) {
+        init = true;
+        if (std::getenv("GAR_HXS_PROF") && hipMalloc(&p, 16 * sizeof(unsigned long long)) == hipSuccess) {
+            (void)hipMemset(p, 0, 16 * sizeof(unsigned long long));
+            (void)hipMemset(p + 10, 0xff, sizeof(unsigned long long));
+            (void)hipMemset(p + 13, 0xff, sizeof(unsigned long long));
+            std::atexit([] {
+                unsigned long long h[16] = {};
+                if (hipDeviceSynchronize() == hipSuccess && hipMemcpy(h, p, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+                    const double nl = h[3] ? static_cast<double>(h[3]) : 1, nc = h[6] ? static_cast<double>(h[6]) : 1;
+                    fprintf(stderr, "hxs prof per wave (cycles): loaders convert %.0f load-issue %.0f barrier %.0f prologue %.0f total %.0f (real %.1f us, clock %.2f GHz) | compute mfma %.0f barrier %.0f\n",
+                            h[0] / nl, h[1] / nl, h[2] / nl, h[7] / nl, h[8] / nl, h[9] / nl / 100.0,
+                            h[9] ? static_cast<double>(h[8]) / static_cast<double>(h[9]) * 0.1 : 0.0, h[4] / nc, h[5] / nc);
+                    fprintf(stderr, "hxs span (last launch ~): first start -> last end %.1f us, latest start %.1f us; loader wave life min %.1f max %.1f us; WGs > 200 us: %llu\n",
+                            (h[11] - h[10]) / 100.0, (h[12] - h[10]) / 100.0, h[13] / 100.0, h[14] / 100.0, h[15]);
+                }
+            });
+        }
+    }
+    return p;
+}
+
+int64_t fdiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
+
+template <int NS>
+hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    switch (x.vst) {
+        case 0: return hxsLaunch<NS, 0>(x, lds, blocks, st);
+        case 1: return hxsLaunch<NS, 1>(x, lds, blocks, st);
+        case 2: return hxsLaunch<NS, 2>(x, lds, blocks, st);
+        default: return hxsLaunch<NS, 3>(x, lds, blocks, st);
+    }
+}
+}  // namespace
+
+// LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B),
+// loader raw slots [loader][2 buffers][slotBytes].
+static size_t hxsLds(int Rt, int slotBytes) {
+    return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256 + static_cast<size_t>(kHxsLoaders) * 2 * slotBytes;
+}
+
+hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
+    if (od.o_hi <= od.o_lo) return hipSuccess;
+    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return hipErrorInvalidConfiguration;
+    static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
+    static const int knobWg = std::getenv("GAR_HXS_WGPERCU") ? std::atoi(std::getenv("GAR_HXS_WGPERCU")) : 0;
+    static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
+    static const int knobDbg = std::getenv("GAR_HXS_DBG") ? std::atoi(std::getenv("GAR_HXS_DBG")) : 0;
+    const int64_t Pc = p.Pc, Qc = p.Qc;
+    const int64_t a_lo = fdiv(od.o_lo, Pc), a_hi = cdiv(od.o_hi, Pc);
+    const int64_t nmac = a_hi - a_lo;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+
+    // chunk length: about one block (16 columns) per CU
+    const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
+    const int64_t nchunkT = std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
+    int64_t Np = std::max<int64_t>(1, cdiv(nmac, nchunkT));
+    int64_t nchunk = cdiv(nmac, Np);
+    // whole blocks where the channel count divides 16 (empty trailing chunks read zeros, store nothing)
+    if (16 % C == 0) nchunk = cdiv(nchunk * C, 16) * 16 / C;
+    const int64_t ncols = nchunk * C;
+    if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorInvalidConfiguration;
+
+    // group size: largest G <= 3 (loader items, LDS) not above Np
+    auto ringFor = [&](int G, int& R, int& Rt, int& Wg) {
+        const int GQ = G * static_cast<int>(Qc);
+        Wg = (G - 1) * static_cast<int>(Qc) + p.Kread;
+        const int n = (Wg + GQ + GQ - 1) / GQ;
+        R = n * GQ;
+        // rows incl. the mirror, rounded to 16 so the quad stride 16*Rt + 64 is 64 mod 256 B:
+        // the four quads of a transposed read land on distinct banks
+        Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
+    };
+    // loader layout: STEREO pieces (32 rows x 8 chunks, LDS-DMA dword), ROW16 pieces (16 rows x 16
+    // channels, LDS-DMA dwordx4) or gathered ROW16 pieces for any other layout
+    const uintptr_t inA = reinterpret_cast<uintptr_t>(src.in);
+    int fmt = 0;
+    if ((inA & 3) == 0 && C == 2 && src.in_fs == 2 && src.in_cs == 1) fmt = 1;
+    else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) fmt = 2;
+    const int RPc = fmt == 1 ? 128 : 16, pieceBytes = fmt == 1 ? 8192 : 1024;
+    auto slotFor = [&](int G) { return ((G * static_cast<int>(Qc) + RPc - 1) / RPc + kHxsLoaders - 1) / kHxsLoaders * pieceBytes; };
+    int G = 1, R = 0, Rt = 0, Wg = 0;
+    for (int cand = 3; cand >= 1; --cand) {
+        int r, rt, wg;
+        ringFor(cand, r, rt, wg);
+        const int dmas = (fmt == 1 ? 8 : 1) * (slotFor(cand) / pieceBytes);
+        if (cand > 1 && (cand > Np || dmas > 32 || hxsLds(rt, slotFor(cand)) > 160 * 1024)) continue;
+        if (knobG > 0 && cand > knobG) continue;
+        G = cand; R = r; Rt = rt; Wg = wg;
+        break;
+    }
+    const int slotBytes = slotFor(G);
+    if (hxsLds(Rt, slotBytes) > 160 * 1024 || (fmt == 1 ? 8 : 1) * (slotBytes / pieceBytes) > 32) return hipErrorInvalidConfiguration;
+
+    HxsArgs x{};
+    x.A = static_cast<const h8v*>(p.A);
+    x.progs = p.progs;
+    x.ea = p.ea;
+    x.Pc = p.Pc; x.Qc = p.Qc; x.Kc = p.Kc; x.Kread = p.Kread; x.G = G; x.C = C;
+    x.nprog = p.nw;
+    x.ncols = static_cast<int>(ncols);
+    x.nblocks = static_cast<int>((ncols + 15) / 16);
+    x.Np = static_cast<int>(Np);
+    x.ngroups = static_cast<int>(cdiv(Np, G));
+    x.R = R; x.Rt = Rt; x.mirror = std::max(0, Wg - G * static_cast<int>(Qc)); x.Wg = Wg;
+    x.a_lo = a_lo; x.a_hi = a_hi;
+    x.dbg = knobDbg;
+    x.prof = profBuf();
+    x.o_lo = od.o_lo; x.o_hi = od.o_hi;
+    // raw input: element (t, c) at in + t*in_fs + c*in_cs for t in [fastLo, fastHi) (integer arithmetic:
+    // the base may point outside the caller's buffer, only rows inside it are dereferenced)
+    const bool rawOk = src.in && !src.in_f64 && src.in_len > 0 && src.in_fs > 0 && src.in_cs >= 0 &&
+                       static_cast<double>(G * Qc + 64) * static_cast<double>(src.in_fs) * 4.0 < 2.0e9;
+    x.in = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(src.in) -
+                                          static_cast<uintptr_t>(src.in_base * src.in_fs * 4));
+    x.in_fs = src.in_fs;
+    x.in_cs = src.in_cs;
+    x.fastLo = rawOk ? src.in_base : 0;
+    x.fastHi = rawOk ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
+    x.fmt = fmt;
+    x.pieceBytes = pieceBytes;
+    x.slotBytes = slotBytes;
+    // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
+    const int esz = od.f64 ? 8 : 4;
+    x.out_f64 = od.f64;
+    x.out = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(od.out) - static_cast<uintptr_t>(od.o0 * od.fs * esz));
+    x.out_fs = od.fs * esz;
+    x.out_cs = od.cs * esz;
+    const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
+    if (od.f64) x.vst = 3;
+    else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;
+    else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;
+    else x.vst = 0;
+    x.src = src;
+    x.od = od;
+    x.rows = p.rows;
+    x.rowOff = p.rowOff;
+    x.rowLen = p.rowLen;
+    x.rowMax = p.rowMax;
+    x.twoStage = p.twoStage;
+    x.rowPh = p.rowPh;
+    x.rowPar = p.rowPar;
+    x.polyA = p.polyA;
+    x.dftC = p.dftC;
+    x.T1 = p.T1;
+    x.T2 = p.T2;
+    if (trace)
+        fprintf(stderr, "hxs: o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
+                (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
+                (long long)x.fastLo, (long long)x.fastHi);
+    const size_t lds = hxsLds(Rt, slotBytes);
+    const int64_t blocks = x.nblocks;
+    switch (p.NS) {
+#define GAR_HXS_NS(n) case n: return hxsVst<n>(x, lds, blocks, stream);
+        GAR_HXS_NS(1) GAR_HXS_NS(2) GAR_HXS_NS(3) GAR_HXS_NS(4) GAR_HXS_NS(5) GAR_HXS_NS(6) GAR_HXS_NS(7)
+        GAR_HXS_NS(8) GAR_HXS_NS(9) GAR_HXS_NS(10)
+#undef GAR_HXS_NS
+        default: return hipErrorInvalidConfiguration;
+    }
+}
+
+}  // namespace gar

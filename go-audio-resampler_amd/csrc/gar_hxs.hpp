@@ -1,0 +1,586 @@
+// gar_hxs.hpp -- streaming split-f16 FIR kernel (row-block plans, gfx950).
+//
+// Same arithmetic as hx_kernel (gar_hx.hpp: constant split scale, three f16
+// MFMA products per 32-deep step, lo products in their own accumulator), so
+// the two kernels produce identical bits; the difference is the data flow:
+//
+//  * Wave specialisation.  Waves [0, nprog) are compute waves: each owns one
+//    row block (A in registers for the whole kernel), reads B fragments from
+//    LDS with ds_read_b64_tr_b16, runs the MFMAs and stores its outputs.  They
+//    issue no global loads, so no s_waitcnt on vector memory ever stalls an
+//    MFMA stream (on gfx950 stores and loads share vmcnt).  The last
+//    kHxsLoaders waves are loader waves: they stream the input rows into LDS,
+//    convert them to the f16 hi/lo split and detect loud elements.
+//  * Long columns.  A column is (channel, chunk of Np consecutive macro
+//    periods); a workgroup owns 16 columns and walks them group by group (G
+//    periods per group, one barrier per group).  Each column's window lives
+//    in an LDS ring of R = n*G*Qc rows (+ a mirror of the first Kread - Qc
+//    rows, so every group's window is contiguous), so each input row is staged
+//    once per column instead of once per G-period window (round-1 kernel:
+//    W/(G*Qc) = 1.34x; here (Np*Qc + Kread - Qc)/(Np*Qc) ~ 1.02x).
+//  * Loud elements (|x| >= 16, Inf, NaN) are staged as zero and their
+//    column-relative row range recorded; after the block, every output whose
+//    window holds one is recomputed exactly (hxExactT: f64, two stages when
+//    non-finite) by the same workgroup.
+#pragma once
+#include <climits>
+
+#include "gar_hx.hpp"
+
+namespace gar {
+
+constexpr int kHxsLoaders = 4;                          // loader waves per workgroup
+constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (3 waves per SIMD)
+
+struct HxsArgs {
+    const h8v* A;          // [nprog][NS][2][64] f16x8
+    const int* progs;      // [nprog][kBgProgInts]
+    int ea, Pc, Qc, Kc, Kread, G, C, nprog;
+    int ncols, nblocks, Np, ngroups;
+    int R, Rt, mirror;     // ring rows (n*G*Qc), rows incl. mirror, mirrored ring rows [0, mirror)
+    int Wg;                // rows one group reads: (G-1)*Qc + Kread
+    unsigned long long* prof;  // development: per-phase cycle sums (GAR_HXS_PROF), null in production
+    int dbg;               // development attribution knob (GAR_HXS_DBG): 1 no loads, 2 no conversion, 4 no MFMA, 8 no stores,
+                           // 16 no mirror writes, 32 no loud marking, 64 no ring writes
+    int pieceBytes, slotBytes;  // loader LDS: bytes per piece, per loader per stage buffer
+    int vst, fmt;          // epilogue layout (template VST), loader format 0 dword / 1 stereo frames / 2 four channels
+    int64_t a_lo, a_hi;    // absolute macro periods of the launch
+    int64_t o_lo, o_hi;    // outputs written
+    const float* in;       // f32 input element (t, c) at in + t*in_fs + c*in_cs, t absolute, raw loads for t in [fastLo, fastHi)
+    int64_t in_fs, in_cs, fastLo, fastHi;
+    char* out;             // output (o, c) at out + o*out_fs + c*out_cs (bytes), o absolute
+    int64_t out_fs, out_cs;
+    int out_f64;
+    // cold fields: edge gathers and the exact fallback (hxExactT)
+    SrcDesc src;
+    OutDesc od;
+    const double* rows;
+    const int* rowOff;
+    const int* rowLen;
+    int rowMax;
+    int twoStage;
+    const int* rowPh;
+    const int* rowPar;
+    const double* polyA;
+    const double* dftC;
+    int T1, T2;
+};
+typedef const __attribute__((address_space(4))) HxsArgs* HxsArgsP;
+
+// Workgroup barrier for LDS hand-offs only: LDS operations drained
+// (lgkmcnt(0)), no vector-memory wait.  __syncthreads() is a release/acquire
+// fence and waits vmcnt(0): the loader waves' prefetch loads and the compute
+// waves' output stores would both drain at every group.
+__device__ __forceinline__ void hxsBarrier() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt max, expcnt max, lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+__device__ __forceinline__ HxsArgsP hxsCold() {
+    uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(v));
+    return reinterpret_cast<HxsArgsP>(v);
+}
+
+// Exact value of output (a, r) of channel c (see hxExact in gar_hx.hpp).
+__device__ __forceinline__ double hxsExact(HxsArgsP x, int64_t a, int r, int c) {
+    const SrcDesc src = kload(&x->src);
+    const int64_t t = a * x->Qc + x->rowOff[r];
+    const int len = x->rowLen[r];
+    const double* row = x->rows + static_cast<size_t>(r) * x->rowMax;
+    double s = 0.0, z = 0.0;
+    for (int k = 0; k < len; ++k) {
+        const double v = static_cast<double>(srcRead<float>(src, t + k, c));
+        s += row[k] * v;
+        z += v * 0.0;
+    }
+    if (z == z || !x->twoStage) return s;
+    const int ph = x->rowPh[r], par = x->rowPar[r], T1 = x->T1, T2 = x->T2;
+    const double* pa = x->polyA + static_cast<size_t>(ph) * T2;
+    double y = 0.0;
+    for (int k2 = 0; k2 < T2; ++k2) {
+        const int q = par + k2;
+        const double* cq = x->dftC + static_cast<size_t>(q & 1) * T1;
+        double u = 0.0;
+        for (int k1 = 0; k1 < T1; ++k1) u += cq[k1] * static_cast<double>(srcRead<float>(src, t + (q >> 1) + k1, c));
+        y += pa[k2] * u;
+    }
+    return y;
+}
+
+// After a block: recompute every output whose window intersects a column's loud
+// row range and really holds a loud element (all threads; out of line).
+__device__ __forceinline__ void hxsFixup(HxsArgsP xp, int b, const int* loudLo, const int* loudHi) {
+    const SrcDesc src = kload(&xp->src);
+    const OutDesc od = kload(&xp->od);
+    const int Pc = xp->Pc, Qc = xp->Qc, Np = xp->Np, C = xp->C, ncols = xp->ncols;
+    const int64_t a_lo = xp->a_lo, a_hi = xp->a_hi;
+    for (int j = 0; j < 16; ++j) {
+        const int lo = loudLo[j], hi = loudHi[j];
+        const int col = b * 16 + j;
+        if (hi < 0 || col >= ncols) continue;
+        const int k = col / C, c = col - k * C;
+        const int p0 = max(0, (lo - xp->Kread) / Qc), p1 = min(Np - 1, hi / Qc);
+        const int n = (p1 - p0 + 1) * Pc;
+        for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
+            const int p = p0 + idx / Pc, r = idx - (idx / Pc) * Pc;
+            const int64_t a = a_lo + static_cast<int64_t>(k) * Np + p;
+            if (a >= a_hi) continue;
+            const int64_t o = a * Pc + r;
+            if (o < od.o_lo || o >= od.o_hi) continue;
+            const int w0 = p * Qc + xp->rowOff[r], w1 = w0 + xp->rowLen[r];
+            if (w1 <= lo || w0 > hi) continue;
+            const int64_t t0 = a * Qc + xp->rowOff[r];
+            bool loud = false;
+            for (int kk = 0; kk < w1 - w0 && !loud; ++kk) loud = hxLoud(srcRead<float>(src, t0 + kk, c));
+            if (loud) outWrite<float>(od, o, c, static_cast<float>(hxsExact(xp, a, r, c)));
+        }
+    }
+}
+
+// ---- loaders ------------------------------------------------------------------
+// A stage (rows [T0, T0 + nrow) of every column) is cut into pieces; loader
+// wave w owns pieces w, w + NL, ...: it moves their raw f32 into its own LDS
+// slots with LDS-DMA (no registers, no cross-wave hand-off), waits for its own
+// DMAs with vmcnt and converts the slots into the ring.  Two layouts:
+//  * STEREO (fmt 1, C == 2): a piece is 128 rows of the 8 chunks of the
+//    block, slot [chunk][row][2 channels]; one buffer_load_dwordx4 ... lds per
+//    chunk (64 lanes = 128 frames, 1 KiB contiguous); a lane converts rows
+//    lane and lane + 64 of every quad.
+//  * ROW16 (fmt 2 with C % 16 == 0: 16 channels of one chunk per block; and
+//    every other layout, gathered): a piece is 16 rows x 16 columns, slot
+//    [row][16]; one buffer_load_dwordx4 ... lds (lane = (row, quad)); lane l
+//    converts row l >> 2, quad l & 3.
+// Rows past the caller's input read zeros through the buffer records; rows
+// before it (history seam, stream start) take the gather path into the same
+// slots.
+struct HxsStage {
+    int T0, nrow;   // column-relative first row and row count
+    bool fast;      // raw loads: every column live, no row before the raw f32 input
+};
+
+__device__ __forceinline__ int hxsPieceRows(const HxsArgs& x) { return x.fmt == 1 ? 128 : 16; }
+
+// Buffer resource over the raw input from absolute row `row0` of channel
+// offset `cofs` (elements): records end at row fastHi, so loads past the
+// caller's input (the tail of the last chunk) read zeros.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxsRsrc(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
+    const float* base = x.in + row0 * x.in_fs + cofs;
+    const int64_t nb = x.fastHi > row0 ? (x.fastHi - row0 - 1) * x.in_fs * 4 + elemBytes : 0;
+    const int nrec = static_cast<int>(nb < 0x7fffffff ? nb : 0x7fffffff);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, nrec, 0x00020000);
+}
+
+// Element (t, c) of the stream for edge stages: history | input (f32/f64) |
+// zero.  Branch-free address selection (a dummy readable address for zeros)
+// so a piece's gathers issue together instead of one dependent load each.
+__device__ __forceinline__ float hxsGather(const SrcDesc& s, int64_t t, int c, const void* dummy) {
+    const int64_t h = t - s.hist_base, i = t - s.in_base;
+    const bool valid = t >= 0 && t < s.valid_end;
+    const bool inH = valid && s.hist && h >= 0 && h < s.hist_len;
+    const bool inI = valid && !inH && s.in && i >= 0 && i < s.in_len;
+    const float* hp = static_cast<const float*>(s.hist) + (inH ? h * s.hist_ld + c : 0);
+    if (s.in_f64) {
+        const double* ip = static_cast<const double*>(s.in) + (inI ? i * s.in_fs + static_cast<int64_t>(c) * s.in_cs : 0);
+        const float vh = *(inH ? hp : static_cast<const float*>(dummy));
+        const double vi = *(inI ? ip : static_cast<const double*>(dummy));
+        return inH ? vh : (inI ? static_cast<float>(vi) : 0.f);
+    }
+    const float* ip = static_cast<const float*>(s.in) + (inI ? i * s.in_fs + static_cast<int64_t>(c) * s.in_cs : 0);
+    const float v = *(inH ? hp : (inI ? ip : static_cast<const float*>(dummy)));
+    return (inH || inI) ? v : 0.f;
+}
+
+__device__ __forceinline__ int64_t hxsChunkRow(const HxsArgs& x, int k, int T0) {
+    return (x.a_lo + static_cast<int64_t>(k) * x.Np) * x.Qc + T0;
+}
+
+// Issue (fast stage) or gather (edge stage) this wave's pieces of a stage into
+// slot base `slots`; returns the number of LDS-DMA instructions issued.
+__device__ __forceinline__ int hxsFetch(const HxsArgs& x, const HxsStage& st, int b, int wl, int lane, char* slots) {
+    const int RPc = hxsPieceRows(x);
+    const int npc = (st.nrow + RPc - 1) / RPc;
+    int nd = 0;
+    if (st.fast && x.fmt == 1) {
+        const int k0 = (b * 16) >> 1;  // first chunk of the block
+        for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
+            char* slot = slots + s * x.pieceBytes;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const __amdgpu_buffer_rsrc_t rs = hxsRsrc(x, hxsChunkRow(x, k0 + k, st.T0 + pc * 128), 0, 8);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + k * 1024), 16,
+                                                         lane * 16, 0, 0, 0);
+            }
+            nd += 8;
+        }
+        return nd;
+    }
+    if (st.fast && x.fmt == 2) {
+        const int col0 = b * 16, k = col0 / x.C, c0 = col0 - k * x.C;
+        const int fsB = static_cast<int>(x.in_fs) * 4;
+        for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
+            const __amdgpu_buffer_rsrc_t rs = hxsRsrc(x, hxsChunkRow(x, k, st.T0 + pc * 16), c0, 64);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slots + s * x.pieceBytes), 16,
+                                                     (lane >> 2) * fsB + (lane & 3) * 16, 0, 0, 0);
+            ++nd;
+        }
+        return nd;
+    }
+    // gathered pieces: edge stages, and every layout without an LDS-DMA form
+    const HxsArgsP xc = hxsCold();
+    const SrcDesc src = kload(&xc->src);
+    const void* dummy = x.A;
+    for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
+        char* slot = slots + s * x.pieceBytes;
+        if (x.fmt == 1) {  // STEREO slot: lane -> rows lane and lane + 64 of each chunk, both channels
+            const int k0 = (b * 16) >> 1;
+#pragma unroll 1
+            for (int k = 0; k < 8; ++k) {
+                f32x4 e = {0.f, 0.f, 0.f, 0.f};
+                if (b * 16 + 2 * k < x.ncols) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        e[i] = hxsGather(src, hxsChunkRow(x, k0 + k, st.T0 + pc * 128 + (i >> 1) * 64 + lane), i & 1, dummy);
+                }
+                *reinterpret_cast<f2v*>(slot + k * 1024 + lane * 8) = f2v{e[0], e[1]};
+                *reinterpret_cast<f2v*>(slot + k * 1024 + 512 + lane * 8) = f2v{e[2], e[3]};
+            }
+        } else {  // ROW16 slot: lane -> (row lane >> 2, quad lane & 3)
+            f32x4 e;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int col = b * 16 + 4 * (lane & 3) + n;
+                const int k = col / x.C, c = col - k * x.C;
+                e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + pc * 16 + (lane >> 2)), c, dummy) : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(slot + lane * 16) = e;
+        }
+    }
+    return 0;
+}
+
+// s_waitcnt vmcnt(n) for a runtime n (the loader's DMAs of the stage just issued).
+__device__ __forceinline__ void hxsWaitVm(int n) {
+#define GAR_VM(v) case v: __builtin_amdgcn_s_waitcnt(((v) & 15) | (((v) >> 4) << 14) | 0x0F70); break;
+    switch (n) {
+        GAR_VM(0) GAR_VM(1) GAR_VM(2) GAR_VM(3) GAR_VM(4) GAR_VM(5) GAR_VM(6) GAR_VM(7) GAR_VM(8) GAR_VM(9)
+        GAR_VM(10) GAR_VM(11) GAR_VM(12) GAR_VM(13) GAR_VM(14) GAR_VM(15) GAR_VM(16) GAR_VM(17) GAR_VM(18)
+        GAR_VM(19) GAR_VM(20) GAR_VM(21) GAR_VM(22) GAR_VM(23) GAR_VM(24) GAR_VM(25) GAR_VM(26) GAR_VM(27)
+        GAR_VM(28) GAR_VM(29) GAR_VM(30) GAR_VM(31) GAR_VM(32)
+        default: __builtin_amdgcn_s_waitcnt(0x0F70); break;
+    }
+#undef GAR_VM
+}
+
+// Loader: one item's 4 values (row `row` of the stage, quad q) -> ring rows
+// (hi/lo split, mirror, loud marking).
+__device__ __forceinline__ void hxsPutItem(const HxsArgs& x, const HxsStage& st, int p0, int q, int row, f32x4 e,
+                                           char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
+    const int t = st.T0 + row;  // column-relative row
+    int p = p0 + row;           // ring row (nrow <= R)
+    if (p >= x.R) p -= x.R;
+    const bool l0 = hxLoud(e[0]), l1 = hxLoud(e[1]), l2 = hxLoud(e[2]), l3 = hxLoud(e[3]);
+    if (__builtin_expect(l0 | l1 | l2 | l3, 0)) {
+        if (l0) { atomicMin(loudLo + 4 * q, t); atomicMax(loudHi + 4 * q, t); e[0] = 0.f; }
+        if (l1) { atomicMin(loudLo + 4 * q + 1, t); atomicMax(loudHi + 4 * q + 1, t); e[1] = 0.f; }
+        if (l2) { atomicMin(loudLo + 4 * q + 2, t); atomicMax(loudHi + 4 * q + 2, t); e[2] = 0.f; }
+        if (l3) { atomicMin(loudLo + 4 * q + 3, t); atomicMax(loudHi + 4 * q + 3, t); e[3] = 0.f; }
+        *flag = 1;
+    }
+    uint2 hv, lv;
+    hxSplit2(e[0], e[1], hv.x, lv.x);
+    hxSplit2(e[2], e[3], hv.y, lv.y);
+    char* qb = ring + q * QS;
+    *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
+    *reinterpret_cast<uint2*>(qb + 8 * x.Rt + 8 * p) = lv;
+    if (p < x.mirror) {
+        p += x.R;
+        *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
+        *reinterpret_cast<uint2*>(qb + 8 * x.Rt + 8 * p) = lv;
+    }
+}
+
+// Loader: this wave's slots of a stage -> ring.
+__device__ __forceinline__ void hxsConvert(const HxsArgs& x, const HxsStage& st, int wl, int lane, const char* slots,
+                                           char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
+    const int RPc = hxsPieceRows(x);
+    const int npc = (st.nrow + RPc - 1) / RPc;
+    const int p0 = uni(st.T0 % x.R);  // ring row of the stage's first row
+    for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
+        const char* slot = slots + s * x.pieceBytes;
+        if (x.fmt == 1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = h * 64 + lane, row = pc * 128 + r;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f2v a = *reinterpret_cast<const f2v*>(slot + (2 * q) * 1024 + r * 8);
+                    const f2v c = *reinterpret_cast<const f2v*>(slot + (2 * q + 1) * 1024 + r * 8);
+                    if (row < st.nrow) hxsPutItem(x, st, p0, q, row, f32x4{a.x, a.y, c.x, c.y}, ring, QS, loudLo, loudHi, flag);
+                }
+            }
+        } else {
+            const int row = pc * 16 + (lane >> 2), q = lane & 3;
+            const f32x4 e = *reinterpret_cast<const f32x4*>(slot + lane * 16);
+            if (row < st.nrow) hxsPutItem(x, st, p0, q, row, e, ring, QS, loudLo, loudHi, flag);
+        }
+    }
+}
+
+// Stage k of a block: k = 0 rows [0, Wg), k >= 1 rows [Wg + (k-1)*G*Qc, Wg + k*G*Qc).
+__device__ __forceinline__ HxsStage hxsStage(const HxsArgs& x, int b, int T0, int nrow) {
+    HxsStage s;
+    s.T0 = T0;
+    s.nrow = nrow;
+    const int c0 = b * 16, c1 = c0 + 15;
+    const int64_t kmin = c0 / x.C;
+    // rows past the raw input read zeros through the buffer records (hxsRsrc);
+    // rows before it (history, stream start), partial blocks and layouts
+    // without an LDS-DMA form are gathered
+    const int64_t tlo = (x.a_lo + kmin * x.Np) * x.Qc + T0;
+    s.fast = (x.fmt == 1 || (x.fmt == 2 && x.C % 16 == 0)) && c1 < x.ncols && tlo >= x.fastLo && x.fastHi > x.fastLo;
+    return s;
+}
+
+template <int VST>
+__device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y, int lane) {
+    if (VST == 2) {
+        const bool even = (lane & 1) == 0;
+        const float s0 = even ? y[2] : y[0], s1 = even ? y[3] : y[1];
+        const float q0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xf, 0xf, false));
+        const float q1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xf, 0xf, false));
+        f32x4 w;
+        if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
+        else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
+        *reinterpret_cast<f32x4*>(p) = w;
+    } else if (VST == 1) {
+        *reinterpret_cast<f32x4*>(p) = y;
+    } else if (VST == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<double*>(p + i * x.out_fs) = static_cast<double>(y[i]);
+    }
+}
+
+// Compute waves (one row block each).  The barrier sequence per block --
+// reset, prologue, one per group, [fixup] -- matches hxsLoaders exactly: the
+// two roles run in separate loops so their registers (A vs raw rows) never
+// live at the same time.
+template <int NS, int VST>
+__device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_t QS, const int* loudLo, const int* loudHi,
+                                           const int* flag, int wt, int lane) {
+    const int sh = -(x.ea + kHxXs);
+    const int GQ = x.G * x.Qc;
+    const int grp = lane >> 4, l16 = lane & 15;
+    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+    const int* pt = x.progs + kBgProgInts * wt;
+    const int u0 = uni(pt[4]), rbw = uni(pt[3]);
+    h8v Ah[NS], Al[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
+        Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
+    }
+    const bool fullRb = (rbw + 1) * 16 <= x.Pc;
+    const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
+    const uint32_t pstep = 8u * static_cast<uint32_t>(x.Qc);
+    const int nslot = x.R / GQ;
+    unsigned long long tm = 0, tw = 0;
+
+    for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
+        hxsBarrier();  // loud state reset; the previous block's ring reads done
+        hxsBarrier();  // prologue staged
+        const int col = b * 16 + l16;
+        const bool colOk = col < x.ncols;
+        const int kcol = col / x.C, ccol = col - kcol * x.C;
+        const int64_t aCol = x.a_lo + static_cast<int64_t>(kcol) * x.Np;
+        const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;  // first row of this lane's accumulator
+        // output of relative period p: whole-quad store, or checked elements at the launch edges
+        auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
+            const f32x4 y = hxScale(oA, oL, sh);
+            if (x.dbg & 8) return;
+            const int64_t a = aCol + p;
+            const int64_t o0 = a * x.Pc + oRow0;
+            const bool live = colOk && p < x.Np && a < x.a_hi;
+            if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+                char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
+                hxsStoreFast<VST>(x, pp, y, lane);
+            } else if (live) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t o = o0 + i;
+                    if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi) {
+                        char* pp = x.out + o * x.out_fs + ccol * x.out_cs;
+                        if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
+                        else *reinterpret_cast<float*>(pp) = y[i];
+                    }
+                }
+            }
+        };
+        for (int g = 0; g < x.ngroups; ++g) {
+            const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            const int slot = g % nslot;
+            uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) +
+                          8u * static_cast<uint32_t>(slot * GQ + u0);
+            h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
+            // one period's MFMA program into nA (hi-x products) and nL (lo-x products); the
+            // epilogue of period ep (oA, oL) issues after its first step when epi
+            auto period = [&](f32x4& nA, f32x4& nL, const f32x4& oA, const f32x4& oL, bool epi, int ep, bool last) {
+                asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
+                const uint32_t aL = aH + dL, aN = aH + pstep, aNL = aN + dL;
+                nA = f32x4{0, 0, 0, 0};
+                nL = nA;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int ug = (s + 1) / NS, us = (s + 1) % NS;
+                    h8v bh1 = bh0, bl1 = bl0;
+                    if (!(ug == 1 && last)) {
+                        bh1 = bFragA((ug == 0 ? aH : aN) + 256 * us);
+                        bl1 = bFragA((ug == 0 ? aL : aNL) + 256 * us);
+                    }
+                    nA = mfma16(Ah[s], bh0, nA);
+                    nA = mfma16(Al[s], bh0, nA);
+                    nL = mfma16(Ah[s], bl0, nL);
+                    bh0 = bh1; bl0 = bl1;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (s == (NS > 1 ? 1 : 0) && epi) epilogue(oA, oL, ep);
+                }
+                aH = aN;
+            };
+            const int p0 = g * x.G;
+            if (x.dbg & 4) { hxsBarrier(); continue; }
+            f32x4 a0, a1 = {0, 0, 0, 0}, l0, l1 = a1;
+            // periods in pairs (alternating accumulators): period i's stores issue from
+            // inside period i+1's MFMA stream
+            period(a0, l0, a1, l1, false, 0, x.G == 1);
+            int i = 1;
+            for (; i + 1 < x.G; i += 2) {
+                period(a1, l1, a0, l0, true, p0 + i - 1, false);
+                period(a0, l0, a1, l1, true, p0 + i, i + 1 == x.G - 1);
+            }
+            if (i < x.G) {
+                period(a1, l1, a0, l0, true, p0 + i - 1, true);
+                epilogue(a1, l1, p0 + i);
+            } else {
+                epilogue(a0, l0, p0 + i - 1);
+            }
+            const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            hxsBarrier();  // group done; stage g+1 staged
+            if (x.prof) { tm += t1 - t0; tw += __builtin_amdgcn_s_memtime() - t1; }
+        }
+        if (*flag) {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
+            __syncthreads();
+            hxsFixup(hxsCold(), b, loudLo, loudHi);
+        }
+    }
+    if (x.prof && lane == 0) {
+        atomicAdd(x.prof + 4, tm);
+        atomicAdd(x.prof + 5, tw);
+        atomicAdd(x.prof + 6, 1ull);
+    }
+}
+
+// Loader waves: stage 0 before the first group; during group g the DMAs of
+// stage g+2 are issued first, then the wave waits for its own DMAs of stage
+// g+1 (issued a group earlier) and converts them into the ring.
+__device__ __forceinline__ void hxsLoaders(const HxsArgs& x, char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag,
+                                           char* rawAll, int wl, int lane) {
+    const int GQ = x.G * x.Qc;
+    char* raw[2] = {rawAll + (2 * wl) * x.slotBytes, rawAll + (2 * wl + 1) * x.slotBytes};
+    unsigned long long tc = 0, tl = 0, tb = 0, tp = 0;
+    const unsigned long long tStart = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
+        const unsigned long long tp0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+        if (wl == 0 && lane < 16) { loudLo[lane] = INT_MAX; loudHi[lane] = -1; }
+        if (wl == 0 && lane == 0) *flag = 0;
+        hxsBarrier();  // loud state reset; the previous block's ring reads done
+        for (int T0 = 0; T0 < x.Wg; T0 += GQ) {
+            const HxsStage st = hxsStage(x, b, T0, min(GQ, x.Wg - T0));
+            hxsFetch(x, st, b, wl, lane, raw[0]);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMAs landed
+            hxsConvert(x, st, wl, lane, raw[0], ring, QS, loudLo, loudHi, flag);
+        }
+        if (x.ngroups > 1) hxsFetch(x, hxsStage(x, b, x.Wg, GQ), b, wl, lane, raw[1]);  // stage 1
+        hxsBarrier();  // prologue staged
+        if (x.prof) tp += __builtin_amdgcn_s_memtime() - tp0;
+        for (int g = 0; g < x.ngroups; ++g) {
+            const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            unsigned long long t1 = t0, t2 = t0;
+            if (g + 1 < x.ngroups) {
+                int nd = 0;
+                if (g + 2 < x.ngroups) nd = hxsFetch(x, hxsStage(x, b, x.Wg + (g + 1) * GQ, GQ), b, wl, lane, raw[g & 1]);
+                if (x.prof) t1 = __builtin_amdgcn_s_memtime();
+                hxsWaitVm(nd);  // stage g+1's DMAs (issued during group g-1) landed
+                hxsConvert(x, hxsStage(x, b, x.Wg + g * GQ, GQ), wl, lane, raw[(g + 1) & 1], ring, QS, loudLo, loudHi, flag);
+                if (x.prof) t2 = __builtin_amdgcn_s_memtime();
+            }
+            hxsBarrier();  // group done; stage g+1 staged
+            if (x.prof) {
+                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                tl += t1 - t0; tc += t2 - t1; tb += t3 - t2;
+            }
+        }
+        if (*flag) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            hxsFixup(hxsCold(), b, loudLo, loudHi);
+        }
+    }
+    if (x.prof && lane == 0) {
+        const unsigned long long rEnd = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(x.prof + 0, tc);
+        atomicAdd(x.prof + 1, tl);
+        atomicAdd(x.prof + 2, tb);
+        atomicAdd(x.prof + 3, 1ull);
+        atomicAdd(x.prof + 7, tp);
+        atomicAdd(x.prof + 8, __builtin_amdgcn_s_memtime() - tStart);
+        atomicAdd(x.prof + 9, rEnd - rStart);
+        if (x.nblocks > 16) {
+            atomicMin(x.prof + 10, rStart);
+            atomicMax(x.prof + 11, rEnd);
+            atomicMax(x.prof + 12, rStart);
+            atomicMin(x.prof + 13, rEnd - rStart);
+            atomicMax(x.prof + 14, rEnd - rStart);
+            if (wl == 0) atomicAdd(x.prof + 15, (rEnd - rStart) > 20000ull ? 1ull : 0ull);  // WGs above 200 us
+        }
+    }
+}
+
+template <int NS, int VST>
+__global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
+    char* ring = reinterpret_cast<char*>(smem);
+    int* loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(QS));
+    int* loudHi = loudLo + 16;
+    int* flag = loudHi + 16;
+    char* rawAll = reinterpret_cast<char*>(smem + 4 * static_cast<size_t>(QS) + 256);  // [loader][2][slotBytes]
+    const int lane = threadIdx.x & 63;
+    const int wt = uni(threadIdx.x >> 6);
+    if (wt < x.nprog) hxsCompute<NS, VST>(x, ring, QS, loudLo, loudHi, flag, wt, lane);
+    else hxsLoaders(x, ring, QS, loudLo, loudHi, flag, rawAll, wt - x.nprog, lane);
+}
+
+// Launch (explicitly instantiated in gar_hxs.hip).
+template <int NS, int VST>
+hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>));
+    hipLaunchKernelGGL((hxs_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.nprog + kHxsLoaders)), lds, st, x);
+    return hipGetLastError();
+}
+
+#define GAR_HXS_FOR4(M, NS) M(NS, 0) M(NS, 1) M(NS, 2) M(NS, 3)
+#define GAR_HXS_FOR_LO(M) GAR_HXS_FOR4(M, 1) GAR_HXS_FOR4(M, 2) GAR_HXS_FOR4(M, 3) GAR_HXS_FOR4(M, 4) GAR_HXS_FOR4(M, 5)
+#define GAR_HXS_FOR_HI(M) GAR_HXS_FOR4(M, 6) GAR_HXS_FOR4(M, 7) GAR_HXS_FOR4(M, 8) GAR_HXS_FOR4(M, 9) GAR_HXS_FOR4(M, 10)
+#define GAR_HXS_FOR_ALL(M) GAR_HXS_FOR_LO(M) GAR_HXS_FOR_HI(M)
+#define GAR_HXS_INST(NS, V) template hipError_t hxsLaunch<NS, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+
+}  // namespace gar

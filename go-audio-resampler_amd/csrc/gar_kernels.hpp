@@ -76,6 +76,8 @@ struct PolyDev {
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+// Streaming wave-specialised variant of launchHx for row-block plans (gar_hxs.hip).
+hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
                       hipStream_t stream);
 // dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.

@@ -132,8 +132,8 @@ def lib():
         "gar_flush_f64": (i32, [vp, vp, i64, C.POINTER(i64)]),
         "gar_flush_f32": (i32, [vp, vp, i64, C.POINTER(i64)]),
         "gar_flush_multi_f64": (i32, [vp, vp, i32, i64, vp]),
-        "gar_process_device": (i32, [vp, vp, i32, i64, i64, i64, vp, i32, i64, i64, i64, C.POINTER(i64), vp]),
-        "gar_flush_device": (i32, [vp, vp, i32, i64, i64, i64, C.POINTER(i64), vp]),
+        "gar_process_device": (i32, [vp, vp, i32, i64, i64, i64, i32, vp, i32, i64, i64, i64, C.POINTER(i64), vp]),
+        "gar_flush_device": (i32, [vp, i32, vp, i32, i64, i64, i64, C.POINTER(i64), vp]),
         "gar_device_output_size": (i64, [vp, i64]),
         "gar_device_flush_size": (i64, [vp]),
         "gar_reset": (None, [vp]),
@@ -298,9 +298,13 @@ class Resampler:
 
     # -- device-resident (torch tensors on cuda) --
     def process_device(self, x, out=None, stream=None):
-        """x: [frames, channels] device tensor (float32/float64, any strides).  Returns out[:n]."""
+        """x: [frames, channels] device tensor (float32/float64, any strides).  Returns out[:n].
+        x.shape[1] (and out.shape[1]) must equal Channels (ErrChannelMismatch)."""
         import torch
         assert x.is_cuda and x.dim() == 2
+        if x.shape[1] != self.Channels or (out is not None and out.shape[1] != self.Channels):
+            raise ErrChannelMismatch(f"expected {self.Channels} channels, got {x.shape[1]}"
+                                     + ("" if out is None else f" (out {out.shape[1]})"))
         frames = x.shape[0]
         n = lib().gar_device_output_size(self._h, frames)
         if n < 0:
@@ -312,12 +316,14 @@ class Resampler:
         odt = F64 if out.dtype == torch.float64 else F32
         st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream)
         _check(lib().gar_process_device(self._h, C.c_void_p(x.data_ptr()), dt, x.stride(0), x.stride(1), frames,
-                                        C.c_void_p(out.data_ptr()), odt, out.stride(0), out.stride(1),
+                                        x.shape[1], C.c_void_p(out.data_ptr()), odt, out.stride(0), out.stride(1),
                                         out.shape[0], C.byref(got), st))
         return out[: got.value]
 
     def flush_device(self, out=None, dtype=None, stream=None):
         import torch
+        if out is not None and out.shape[1] != self.Channels:
+            raise ErrChannelMismatch(f"expected {self.Channels} channels, got {out.shape[1]}")
         n = lib().gar_device_flush_size(self._h)
         if n < 0:
             raise ErrNotSupported("channels not in lockstep")
@@ -326,8 +332,8 @@ class Resampler:
         got = C.c_int64(0)
         odt = F64 if out.dtype == torch.float64 else F32
         st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream)
-        _check(lib().gar_flush_device(self._h, C.c_void_p(out.data_ptr()), odt, out.stride(0), out.stride(1),
-                                      out.shape[0], C.byref(got), st))
+        _check(lib().gar_flush_device(self._h, out.shape[1], C.c_void_p(out.data_ptr()), odt, out.stride(0),
+                                      out.stride(1), out.shape[0], C.byref(got), st))
         return out[: got.value]
 
 

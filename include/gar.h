@@ -149,18 +149,26 @@ gar_status gar_flush_multi_f64(gar_resampler *r, double *const *out, int32_t n_c
                                int64_t *n_out);
 
 /* ---- device-resident batched streaming (all channels in lockstep) -------- */
-/* Process `frames` frames of all channels from device memory `in` (dtype
- * in_dtype) into device memory `out`; *out_frames = frames produced per
- * channel.  GAR_ERR_BUFFER_TOO_SMALL (no state change) if out_cap_frames is
- * smaller than the exact output size.  Asynchronous on `stream` (NULL = the
- * default stream); returns once the work is enqueued. */
+/* Process `frames` frames of all `channels` channels (must equal the handle's
+ * channel count: GAR_ERR_CHANNEL_MISMATCH otherwise, like ProcessMulti,
+ * constant.go:205-207) from device memory `in` (dtype in_dtype) into device
+ * memory `out`; *out_frames = frames produced per channel.
+ * GAR_ERR_BUFFER_TOO_SMALL (no state change) if out_cap_frames is smaller than
+ * the exact output size.  Asynchronous on `stream` (NULL = the default
+ * stream); returns once the work is enqueued.  Calls on one handle are
+ * ordered even across streams (each waits for the handle's previous call);
+ * the caller keeps `in` alive and `out` untouched until `stream` has run the
+ * call.  A device error leaves the handle refusing work (GAR_ERR_DEVICE)
+ * until gar_reset.  The handle's device is made current for the call and the
+ * caller's current device restored. */
 gar_status gar_process_device(gar_resampler *r, const void *in, int32_t in_dtype, int64_t in_frame_stride,
-                              int64_t in_channel_stride, int64_t frames, void *out, int32_t out_dtype,
-                              int64_t out_frame_stride, int64_t out_channel_stride, int64_t out_cap_frames,
-                              int64_t *out_frames, void *stream);
-/* Flush all channels into device memory (FlushMulti semantics). */
-gar_status gar_flush_device(gar_resampler *r, void *out, int32_t out_dtype, int64_t out_frame_stride,
-                            int64_t out_channel_stride, int64_t out_cap_frames, int64_t *out_frames, void *stream);
+                              int64_t in_channel_stride, int64_t frames, int32_t channels, void *out,
+                              int32_t out_dtype, int64_t out_frame_stride, int64_t out_channel_stride,
+                              int64_t out_cap_frames, int64_t *out_frames, void *stream);
+/* Flush all channels into device memory (FlushMulti semantics); `channels` as above. */
+gar_status gar_flush_device(gar_resampler *r, int32_t channels, void *out, int32_t out_dtype,
+                            int64_t out_frame_stride, int64_t out_channel_stride, int64_t out_cap_frames,
+                            int64_t *out_frames, void *stream);
 /* Exact lockstep output sizes (-1 if channels are not in lockstep). */
 int64_t gar_device_output_size(const gar_resampler *r, int64_t frames);
 int64_t gar_device_flush_size(const gar_resampler *r);

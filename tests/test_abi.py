@@ -180,3 +180,25 @@ def test_batch_handle_channel_count(gar):
     assert g.Channels == 2048
     with pytest.raises(gar.ErrInvalidConfig):
         gar.NewBatch(gar.Config(44100, 48000, 300, gar.QualityHigh, DryRun=True), 2)
+
+
+def test_device_api_channel_mismatch(gar):
+    """gar_process_device / gar_flush_device refuse a buffer whose channel count is not the
+    handle's (ErrChannelMismatch, constant.go:205-207) before touching memory."""
+    import ctypes as C
+    r = gar.New(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True))
+    got = C.c_int64(0)
+    rc = gar.lib().gar_process_device(r._h, None, gar.F32, 1, 1, 100, 3, None, gar.F32, 1, 1, 1000, C.byref(got), None)
+    assert rc == gar.CHANNEL_MISMATCH
+    rc = gar.lib().gar_flush_device(r._h, 1, None, gar.F32, 1, 1, 1000, C.byref(got), None)
+    assert rc == gar.CHANNEL_MISMATCH
+    rc = gar.lib().gar_process_device(r._h, None, gar.F32, 2, 1, -5, 2, None, gar.F32, 2, 1, 1000, C.byref(got), None)
+    assert rc == gar.INVALID_ARGUMENT
+
+
+def test_engine_quality_constructor_dry(gar):
+    """gar_new_engine_quality maps engine.Quality directly (resampler.go:51): unknown values are ErrInvalidConfig."""
+    import ctypes as C
+    h = C.c_void_p(0)
+    assert gar.lib().gar_new_engine_quality(44100.0, 48000.0, 42, gar.F64, C.byref(h)) == gar.INVALID_CONFIG
+    assert not h.value

@@ -16,8 +16,12 @@ def summarize(d, kernel="hx_kernel"):
     return agg
 
 if __name__ == "__main__":
-    for d in sys.argv[1:]:
-        a = summarize(d)
+    args = sys.argv[1:]
+    kernel = "hx_kernel"
+    if args and args[0] == "--kernel":
+        kernel, args = args[1], args[2:]
+    for d in args:
+        a = summarize(d, kernel)
         w = a.get("SQ_WAVE_CYCLES", 1)
         print(d, json.dumps({k: float(f"{v:.4g}") for k, v in sorted(a.items())}))
         if "SQ_WAIT_ANY" in a:
