@@ -40,7 +40,10 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // row-block plans stream through the wave-specialised kernel (GAR_HXS=0: the block kernel, A/B runs)
     static const bool hxs = !(std::getenv("GAR_HXS") && std::getenv("GAR_HXS")[0] == '0');
-    if (p.rb && hxs) return launchHxs(p, src, od, C, stream);
+    if (p.rb && hxs) {
+        const hipError_t e = launchHxs(p, src, od, C, stream);
+        if (e != hipErrorNotSupported) return e;
+    }
     // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bits: 1 skip
     // staging after the first block, 2 skip the MFMA programs, 16 skip the loop
     static const int knobG = std::getenv("GAR_HX_G") ? std::atoi(std::getenv("GAR_HX_G")) : 0;

@@ -5,6 +5,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
+#include <vector>
 
 #include "gar_hxs.hpp"
 
@@ -16,25 +18,46 @@ GAR_HXS_FOR_ALL(GAR_HXS_EXT)
 #undef GAR_HXS_EXT
 
 namespace {
+constexpr int kProfWords = 64 + 2 * 4096;
 // development: GAR_HXS_PROF=1 sums per-phase s_memtime cycles of every launch and prints them at exit
 unsigned long long* profBuf() {
     static unsigned long long* p = nullptr;
     static bool init = false;
     if (!init) {
         init = true;
-        if (std::getenv("GAR_HXS_PROF") && hipMalloc(&p, 16 * sizeof(unsigned long long)) == hipSuccess) {
-            (void)hipMemset(p, 0, 16 * sizeof(unsigned long long));
+        if (std::getenv("GAR_HXS_PROF") && hipMalloc(&p, kProfWords * sizeof(unsigned long long)) == hipSuccess) {
+            (void)hipMemset(p, 0, kProfWords * sizeof(unsigned long long));
             (void)hipMemset(p + 10, 0xff, sizeof(unsigned long long));
             (void)hipMemset(p + 13, 0xff, sizeof(unsigned long long));
             std::atexit([] {
-                unsigned long long h[16] = {};
+                static unsigned long long h[kProfWords] = {};
                 if (hipDeviceSynchronize() == hipSuccess && hipMemcpy(h, p, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
                     const double nl = h[3] ? static_cast<double>(h[3]) : 1, nc = h[6] ? static_cast<double>(h[6]) : 1;
-                    fprintf(stderr, "hxs prof per wave (cycles): loaders convert %.0f load-issue %.0f barrier %.0f prologue %.0f total %.0f (real %.1f us, clock %.2f GHz) | compute mfma %.0f barrier %.0f\n",
-                            h[0] / nl, h[1] / nl, h[2] / nl, h[7] / nl, h[8] / nl, h[9] / nl / 100.0,
-                            h[9] ? static_cast<double>(h[8]) / static_cast<double>(h[9]) * 0.1 : 0.0, h[4] / nc, h[5] / nc);
-                    fprintf(stderr, "hxs span (last launch ~): first start -> last end %.1f us, latest start %.1f us; loader wave life min %.1f max %.1f us; WGs > 200 us: %llu\n",
-                            (h[11] - h[10]) / 100.0, (h[12] - h[10]) / 100.0, h[13] / 100.0, h[14] / 100.0, h[15]);
+                    fprintf(stderr, "hxs prof per wave (cycles): loaders convert %.0f issue+wait %.0f (issue %.0f) barrier %.0f (life %.1f us) | compute convert+mfma %.0f barrier %.0f\n",
+                            h[0] / nl, h[1] / nl, h[7] / nl, h[2] / nl, h[9] / nl / 100.0, h[4] / nc, h[5] / nc);
+                    fprintf(stderr, "hxs loader pre-loop %.2f us, post-loop %.2f us; compute convert %.0f\n", h[8] / nl / 100.0, h[12] / nl / 100.0, h[15] / nc);
+                    fprintf(stderr, "hxs span: first start -> last end %.1f us; loader wave life min %.1f max %.1f us\n",
+                            (h[11] - h[10]) / 100.0, h[13] / 100.0, h[14] / 100.0);
+                    // per-workgroup life (last launch): percentiles, by blockIdx % 8, slowest
+                    std::vector<std::pair<double, int>> v;
+                    unsigned long long t0 = ~0ull;
+                    for (int b = 0; b < 4096; ++b)
+                        if (h[65 + 2 * b]) { v.push_back({h[65 + 2 * b] / 100.0, b}); t0 = std::min(t0, h[64 + 2 * b]); }
+                    if (!v.empty()) {
+                        std::vector<std::pair<double, int>> sv = v;
+                        std::sort(sv.begin(), sv.end());
+                        auto pc = [&](double q) { return sv[std::min(sv.size() - 1, static_cast<size_t>(q * sv.size()))].first; };
+                        fprintf(stderr, "hxs WG life us: n %zu min %.1f p10 %.1f p50 %.1f p90 %.1f max %.1f |", sv.size(), sv.front().first, pc(0.1), pc(0.5), pc(0.9), sv.back().first);
+                        for (int m = 0; m < 8; ++m) {
+                            double s = 0; int n = 0;
+                            for (auto& e : v) if (e.second % 8 == m) { s += e.first; ++n; }
+                            fprintf(stderr, " x%d %.1f", m, n ? s / n : 0.0);
+                        }
+                        fprintf(stderr, "\n  slowest:");
+                        for (size_t k = sv.size(); k-- > 0 && k + 8 >= sv.size();)
+                            fprintf(stderr, " b%d %.1fus@+%.1f", sv[k].second, sv[k].first, (h[64 + 2 * sv[k].second] - t0) / 100.0);
+                        fprintf(stderr, "\n");
+                    }
                 }
             });
         }
@@ -57,14 +80,15 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 }  // namespace
 
 // LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B),
-// loader raw slots [loader][2 buffers][slotBytes].
-static size_t hxsLds(int Rt, int slotBytes) {
-    return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256 + static_cast<size_t>(kHxsLoaders) * 2 * slotBytes;
+// three raw stage buffers.
+static size_t hxsLds(int Rt, int stageBytes) {
+    return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256 + 3 * static_cast<size_t>(stageBytes);
 }
 
+// hipErrorNotSupported: the plan does not fit this kernel's geometry (the caller uses hx_kernel).
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
-    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return hipErrorInvalidConfiguration;
+    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return hipErrorNotSupported;
     static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
     static const int knobWg = std::getenv("GAR_HXS_WGPERCU") ? std::atoi(std::getenv("GAR_HXS_WGPERCU")) : 0;
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
@@ -79,13 +103,19 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
     const int64_t nchunkT = std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
     int64_t Np = std::max<int64_t>(1, cdiv(nmac, nchunkT));
+    // raw loads address a chunk's rows with 32-bit offsets from the chunk's first row:
+    // (Np*Qc + rows of one group + a piece) rows must span less than 2^31 bytes
+    const int64_t rowBytes = std::max<int64_t>(4, src.in_fs * 4);
+    const int64_t npMax = ((int64_t(1) << 31) / rowBytes - (3 * Qc + p.Kread + 256)) / Qc;
+    const bool rawSpan = npMax >= 1;
+    if (rawSpan) Np = std::min(Np, npMax);
     int64_t nchunk = cdiv(nmac, Np);
     // whole blocks where the channel count divides 16 (empty trailing chunks read zeros, store nothing)
     if (16 % C == 0) nchunk = cdiv(nchunk * C, 16) * 16 / C;
     const int64_t ncols = nchunk * C;
-    if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorInvalidConfiguration;
+    if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorNotSupported;
 
-    // group size: largest G <= 3 (loader items, LDS) not above Np
+    // group size: largest G <= 3 (LDS, DMAs per loader, staged items per thread) not above Np
     auto ringFor = [&](int G, int& R, int& Rt, int& Wg) {
         const int GQ = G * static_cast<int>(Qc);
         Wg = (G - 1) * static_cast<int>(Qc) + p.Kread;
@@ -95,26 +125,32 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         // the four quads of a transposed read land on distinct banks
         Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
     };
-    // loader layout: STEREO pieces (32 rows x 8 chunks, LDS-DMA dword), ROW16 pieces (16 rows x 16
+    // raw stage layout: STEREO pieces (128 rows x 8 chunks, LDS-DMA dwordx4), ROW16 pieces (16 rows x 16
     // channels, LDS-DMA dwordx4) or gathered ROW16 pieces for any other layout
     const uintptr_t inA = reinterpret_cast<uintptr_t>(src.in);
     int fmt = 0;
-    if ((inA & 3) == 0 && C == 2 && src.in_fs == 2 && src.in_cs == 1) fmt = 1;
+    if ((inA & 7) == 0 && C == 2 && src.in_fs == 2 && src.in_cs == 1) fmt = 1;
     else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) fmt = 2;
-    const int RPc = fmt == 1 ? 128 : 16, pieceBytes = fmt == 1 ? 8192 : 1024;
-    auto slotFor = [&](int G) { return ((G * static_cast<int>(Qc) + RPc - 1) / RPc + kHxsLoaders - 1) / kHxsLoaders * pieceBytes; };
-    int G = 1, R = 0, Rt = 0, Wg = 0;
+    const int RPc = fmt == 1 ? 128 : 16, pieceBytes = fmt == 1 ? 8192 : 1024, dmaPerPiece = fmt == 1 ? 8 : 1;
+    auto stageFor = [&](int G) { return (G * static_cast<int>(Qc) + RPc - 1) / RPc * pieceBytes; };
+    const int nth = 64 * (p.nw + kHxsLoaders);
+    auto fits = [&](int G, int Rt) {
+        const int GQ = G * static_cast<int>(Qc);
+        const int dmas = (stageFor(G) / pieceBytes * dmaPerPiece + kHxsLoaders - 1) / kHxsLoaders;
+        return hxsLds(Rt, stageFor(G)) <= 160 * 1024 && 2 * dmas <= 32 && 4 * ((GQ + 63) / 64 * 64) <= kHxsConvMax * nth;
+    };
+    int G = 0, R = 0, Rt = 0, Wg = 0;
     for (int cand = 3; cand >= 1; --cand) {
         int r, rt, wg;
         ringFor(cand, r, rt, wg);
-        const int dmas = (fmt == 1 ? 8 : 1) * (slotFor(cand) / pieceBytes);
-        if (cand > 1 && (cand > Np || dmas > 32 || hxsLds(rt, slotFor(cand)) > 160 * 1024)) continue;
-        if (knobG > 0 && cand > knobG) continue;
+        if (cand > 1 && cand > Np) continue;
+        if (knobG > 0 && cand > knobG && cand > 1) continue;
+        if (!fits(cand, rt)) continue;
         G = cand; R = r; Rt = rt; Wg = wg;
         break;
     }
-    const int slotBytes = slotFor(G);
-    if (hxsLds(Rt, slotBytes) > 160 * 1024 || (fmt == 1 ? 8 : 1) * (slotBytes / pieceBytes) > 32) return hipErrorInvalidConfiguration;
+    if (G == 0) return hipErrorNotSupported;
+    const int stageBytes = stageFor(G);
 
     HxsArgs x{};
     x.A = static_cast<const h8v*>(p.A);
@@ -133,8 +169,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.o_lo = od.o_lo; x.o_hi = od.o_hi;
     // raw input: element (t, c) at in + t*in_fs + c*in_cs for t in [fastLo, fastHi) (integer arithmetic:
     // the base may point outside the caller's buffer, only rows inside it are dereferenced)
-    const bool rawOk = src.in && !src.in_f64 && src.in_len > 0 && src.in_fs > 0 && src.in_cs >= 0 &&
-                       static_cast<double>(G * Qc + 64) * static_cast<double>(src.in_fs) * 4.0 < 2.0e9;
+    const bool rawOk = src.in && !src.in_f64 && src.in_len > 0 && src.in_fs > 0 && src.in_cs >= 0 && rawSpan;
     x.in = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(src.in) -
                                           static_cast<uintptr_t>(src.in_base * src.in_fs * 4));
     x.in_fs = src.in_fs;
@@ -142,8 +177,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.fastLo = rawOk ? src.in_base : 0;
     x.fastHi = rawOk ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
     x.fmt = fmt;
-    x.pieceBytes = pieceBytes;
-    x.slotBytes = slotBytes;
+    x.stageBytes = stageBytes;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
     const int esz = od.f64 ? 8 : 4;
     x.out_f64 = od.f64;
@@ -172,14 +206,14 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         fprintf(stderr, "hxs: o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
                 (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
                 (long long)x.fastLo, (long long)x.fastHi);
-    const size_t lds = hxsLds(Rt, slotBytes);
+    const size_t lds = hxsLds(Rt, stageBytes);
     const int64_t blocks = x.nblocks;
     switch (p.NS) {
 #define GAR_HXS_NS(n) case n: return hxsVst<n>(x, lds, blocks, stream);
         GAR_HXS_NS(1) GAR_HXS_NS(2) GAR_HXS_NS(3) GAR_HXS_NS(4) GAR_HXS_NS(5) GAR_HXS_NS(6) GAR_HXS_NS(7)
         GAR_HXS_NS(8) GAR_HXS_NS(9) GAR_HXS_NS(10)
 #undef GAR_HXS_NS
-        default: return hipErrorInvalidConfiguration;
+        default: return hipErrorNotSupported;
     }
 }
 

@@ -30,7 +30,8 @@
 namespace gar {
 
 constexpr int kHxsLoaders = 4;                          // loader waves per workgroup
-constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (3 waves per SIMD)
+constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 waves per SIMD)
+constexpr int kHxsConvMax = 8;                          // staged items per thread per stage
 
 struct HxsArgs {
     const h8v* A;          // [nprog][NS][2][64] f16x8
@@ -40,10 +41,10 @@ struct HxsArgs {
     int R, Rt, mirror;     // ring rows (n*G*Qc), rows incl. mirror, mirrored ring rows [0, mirror)
     int Wg;                // rows one group reads: (G-1)*Qc + Kread
     unsigned long long* prof;  // development: per-phase cycle sums (GAR_HXS_PROF), null in production
-    int dbg;               // development attribution knob (GAR_HXS_DBG): 1 no loads, 2 no conversion, 4 no MFMA, 8 no stores,
-                           // 16 no mirror writes, 32 no loud marking, 64 no ring writes
-    int pieceBytes, slotBytes;  // loader LDS: bytes per piece, per loader per stage buffer
-    int vst, fmt;          // epilogue layout (template VST), loader format 0 dword / 1 stereo frames / 2 four channels
+    int dbg;               // development attribution (GAR_HXS_DBG, wrong output): 1 no steady DMAs, 2 no stores,
+                           // 4 no MFMA, 16 no steady conversion
+    int stageBytes;        // raw LDS bytes of one stage (three buffers)
+    int vst, fmt;          // epilogue layout (template VST), raw stage layout 0 gathered ROW16 / 1 STEREO / 2 ROW16 DMA
     int64_t a_lo, a_hi;    // absolute macro periods of the launch
     int64_t o_lo, o_hi;    // outputs written
     const float* in;       // f32 input element (t, c) at in + t*in_fs + c*in_cs, t absolute, raw loads for t in [fastLo, fastHi)
@@ -140,37 +141,57 @@ __device__ __forceinline__ void hxsFixup(HxsArgsP xp, int b, const int* loudLo, 
     }
 }
 
-// ---- loaders ------------------------------------------------------------------
-// A stage (rows [T0, T0 + nrow) of every column) is cut into pieces; loader
-// wave w owns pieces w, w + NL, ...: it moves their raw f32 into its own LDS
-// slots with LDS-DMA (no registers, no cross-wave hand-off), waits for its own
-// DMAs with vmcnt and converts the slots into the ring.  Two layouts:
-//  * STEREO (fmt 1, C == 2): a piece is 128 rows of the 8 chunks of the
-//    block, slot [chunk][row][2 channels]; one buffer_load_dwordx4 ... lds per
-//    chunk (64 lanes = 128 frames, 1 KiB contiguous); a lane converts rows
-//    lane and lane + 64 of every quad.
-//  * ROW16 (fmt 2 with C % 16 == 0: 16 channels of one chunk per block; and
-//    every other layout, gathered): a piece is 16 rows x 16 columns, slot
-//    [row][16]; one buffer_load_dwordx4 ... lds (lane = (row, quad)); lane l
-//    converts row l >> 2, quad l & 3.
+// ---- staging --------------------------------------------------------------------
+// A stage (rows [T0, T0 + nrow) of every column of the block) travels:
+//   global --LDS-DMA (loader waves)--> raw buffer --split (every wave)--> ring.
+// Stage k is needed by group k; it is DMA'd during group k-2 into raw buffer
+// k % 3, the loaders' vmcnt wait before the end of group k-1 makes it visible
+// to every wave, and during group k-1 all waves convert their share of it.
+// Raw layouts:
+//  * STEREO (fmt 1, C == 2): pieces of 128 rows x the 8 chunks of the block,
+//    [piece][chunk][row][2 channels]; one buffer_load_dwordx4 ... lds per
+//    (piece, chunk) (64 lanes = 128 frames, 1 KiB contiguous).
+//  * ROW16 (fmt 2 with C % 16 == 0: the 16 columns are 16 channels of one
+//    chunk): pieces of 16 rows, [piece][row][16]; one buffer_load_dwordx4 ...
+//    lds per piece (lane = (row, quad)).
+//  * every other layout: ROW16 pieces gathered through registers.
 // Rows past the caller's input read zeros through the buffer records; rows
-// before it (history seam, stream start) take the gather path into the same
-// slots.
+// before it (history seam, stream start) are gathered.
 struct HxsStage {
     int T0, nrow;   // column-relative first row and row count
-    bool fast;      // raw loads: every column live, no row before the raw f32 input
+    bool fast;      // LDS-DMA: every column live, no row before the raw f32 input
 };
 
-__device__ __forceinline__ int hxsPieceRows(const HxsArgs& x) { return x.fmt == 1 ? 128 : 16; }
-
-// Buffer resource over the raw input from absolute row `row0` of channel
-// offset `cofs` (elements): records end at row fastHi, so loads past the
-// caller's input (the tail of the last chunk) read zeros.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxsRsrc(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
-    const float* base = x.in + row0 * x.in_fs + cofs;
+// Buffer resource (raw, stride 0) over the raw input from absolute row `row0`
+// of channel offset `cofs` (elements): records end at row fastHi, so loads past
+// the caller's input (the tail of the last chunk) read zeros.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4v hxsRsrc(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
+    const uint64_t base = reinterpret_cast<uint64_t>(x.in + row0 * x.in_fs + cofs);
     const int64_t nb = x.fastHi > row0 ? (x.fastHi - row0 - 1) * x.in_fs * 4 + elemBytes : 0;
-    const int nrec = static_cast<int>(nb < 0x7fffffff ? nb : 0x7fffffff);
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, nrec, 0x00020000);
+    const unsigned nrec = static_cast<unsigned>(nb < 0x7fffffff ? nb : 0x7fffffff);
+    u32x4v r;
+    r.x = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(base));
+    r.y = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(base >> 32) & 0xffffu);
+    r.z = __builtin_amdgcn_readfirstlane(nrec);
+    r.w = 0x00020000u;
+    return r;
+}
+
+// One LDS-DMA piece: 64 lanes x 16 B from rsrc + voff (per lane) to LDS
+// [lds, lds + 1 KiB), lane-linear.  Inline asm on purpose: the compiler then
+// does not track the piece as a pending LDS write, so it inserts no vmcnt(0)
+// before every later LDS access of the wave (the conversion's ring writes);
+// the pieces are waited for explicitly (hxsWaitVm) before the barrier that
+// publishes them.
+__device__ __forceinline__ void hxsDma16(u32x4v rs, const void* lds, int voff) {
+    const unsigned a = __builtin_amdgcn_readfirstlane(
+        static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)lds)));
+    unsigned m0save;  // m0 is reserved to the compiler: restored after the issue
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(m0save)
+                 : "v"(voff), "s"(rs), "s"(a)
+                 : "memory");
 }
 
 // Element (t, c) of the stream for edge stages: history | input (f32/f64) |
@@ -197,71 +218,92 @@ __device__ __forceinline__ int64_t hxsChunkRow(const HxsArgs& x, int k, int T0) 
     return (x.a_lo + static_cast<int64_t>(k) * x.Np) * x.Qc + T0;
 }
 
-// Issue (fast stage) or gather (edge stage) this wave's pieces of a stage into
-// slot base `slots`; returns the number of LDS-DMA instructions issued.
-__device__ __forceinline__ int hxsFetch(const HxsArgs& x, const HxsStage& st, int b, int wl, int lane, char* slots) {
-    const int RPc = hxsPieceRows(x);
-    const int npc = (st.nrow + RPc - 1) / RPc;
-    int nd = 0;
-    if (st.fast && x.fmt == 1) {
+// Stage k of a block: k = 0 rows [0, Wg) (in parts of at most G*Qc), k >= 1
+// rows [Wg + (k-1)*G*Qc, Wg + k*G*Qc).
+__device__ __forceinline__ HxsStage hxsStage(const HxsArgs& x, int b, int T0, int nrow) {
+    HxsStage s;
+    s.T0 = T0;
+    s.nrow = nrow;
+    const int c0 = b * 16, c1 = c0 + 15;
+    const int64_t tlo = (x.a_lo + static_cast<int64_t>(c0 / x.C) * x.Np) * x.Qc + T0;
+    s.fast = (x.fmt == 1 || x.fmt == 2) && c1 < x.ncols && tlo >= x.fastLo && x.fastHi > x.fastLo;
+    return s;
+}
+// Load j of a block: j < P = ceil(Wg / GQ) the parts of stage 0 (rows [j*GQ, ...) up to Wg),
+// then stage j - P + 1 (rows [Wg + (j-P)*GQ, + GQ)).
+__device__ __forceinline__ HxsStage hxsLoad(const HxsArgs& x, int b, int j, int P) {
+    const int GQ = x.G * x.Qc;
+    if (j < P) return hxsStage(x, b, j * GQ, min(GQ, x.Wg - j * GQ));
+    return hxsStage(x, b, x.Wg + (j - P) * GQ, GQ);
+}
+
+// Loader wave wl: DMA (fast) or gather (edge) its share of a stage into raw
+// buffer `raw`; returns the number of LDS-DMA instructions it issued.
+__device__ __forceinline__ int hxsIssue(const HxsArgs& x, const HxsStage& st, int b, int wl, int lane, char* raw) {
+    if (x.fmt == 1) {
+        const int npc = (st.nrow + 127) >> 7;
         const int k0 = (b * 16) >> 1;  // first chunk of the block
-        for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
-            char* slot = slots + s * x.pieceBytes;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const __amdgpu_buffer_rsrc_t rs = hxsRsrc(x, hxsChunkRow(x, k0 + k, st.T0 + pc * 128), 0, 8);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slot + k * 1024), 16,
-                                                         lane * 16, 0, 0, 0);
+        if (st.fast) {
+            // this loader's two chunks (wl, wl + 4): one resource each from the chunk's row 0, the
+            // stage's rows as a per-lane offset (in range: Np*Qc + Wg rows fit 31 bits, launcher)
+            const u32x4v rA = hxsRsrc(x, hxsChunkRow(x, k0 + wl, 0), 0, 8);
+            const u32x4v rB = hxsRsrc(x, hxsChunkRow(x, k0 + wl + 4, 0), 0, 8);
+            const int rowB = static_cast<int>(x.in_fs) * 4;
+            int voff = st.T0 * rowB + lane * 16;
+            char* dst = raw + wl * 1024;
+            for (int pc = 0; pc < npc; ++pc) {
+                hxsDma16(rA, dst, voff);
+                hxsDma16(rB, dst + 4096, voff);
+                voff += 128 * rowB;
+                dst += 8192;
             }
-            nd += 8;
+            return 2 * npc;
         }
-        return nd;
+        const HxsArgsP xc = hxsCold();
+        const SrcDesc src = kload(&xc->src);
+        for (int d = wl; d < npc * 8; d += kHxsLoaders) {
+            const int pc = d >> 3, k = d & 7;
+            f32x4 e = {0.f, 0.f, 0.f, 0.f};
+            if (b * 16 + 2 * k < x.ncols) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    e[i] = hxsGather(src, hxsChunkRow(x, k0 + k, st.T0 + pc * 128 + (i >> 1) * 64 + lane), i & 1, x.A);
+            }
+            *reinterpret_cast<f2v*>(raw + d * 1024 + lane * 8) = f2v{e[0], e[1]};
+            *reinterpret_cast<f2v*>(raw + d * 1024 + 512 + lane * 8) = f2v{e[2], e[3]};
+        }
+        return 0;
     }
-    if (st.fast && x.fmt == 2) {
+    const int npc = (st.nrow + 15) >> 4;
+    if (st.fast) {  // fmt 2: 16 channels of one chunk
         const int col0 = b * 16, k = col0 / x.C, c0 = col0 - k * x.C;
         const int fsB = static_cast<int>(x.in_fs) * 4;
-        for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
-            const __amdgpu_buffer_rsrc_t rs = hxsRsrc(x, hxsChunkRow(x, k, st.T0 + pc * 16), c0, 64);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(slots + s * x.pieceBytes), 16,
-                                                     (lane >> 2) * fsB + (lane & 3) * 16, 0, 0, 0);
+        const u32x4v rs = hxsRsrc(x, hxsChunkRow(x, k, 0), c0, 64);
+        int voff = (st.T0 + wl * 16 + (lane >> 2)) * fsB + (lane & 3) * 16;
+        int nd = 0;
+        for (int pc = wl; pc < npc; pc += kHxsLoaders) {
+            hxsDma16(rs, raw + pc * 1024, voff);
+            voff += kHxsLoaders * 16 * fsB;
             ++nd;
         }
         return nd;
     }
-    // gathered pieces: edge stages, and every layout without an LDS-DMA form
     const HxsArgsP xc = hxsCold();
     const SrcDesc src = kload(&xc->src);
-    const void* dummy = x.A;
-    for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
-        char* slot = slots + s * x.pieceBytes;
-        if (x.fmt == 1) {  // STEREO slot: lane -> rows lane and lane + 64 of each chunk, both channels
-            const int k0 = (b * 16) >> 1;
-#pragma unroll 1
-            for (int k = 0; k < 8; ++k) {
-                f32x4 e = {0.f, 0.f, 0.f, 0.f};
-                if (b * 16 + 2 * k < x.ncols) {
+    for (int pc = wl; pc < npc; pc += kHxsLoaders) {
+        f32x4 e;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        e[i] = hxsGather(src, hxsChunkRow(x, k0 + k, st.T0 + pc * 128 + (i >> 1) * 64 + lane), i & 1, dummy);
-                }
-                *reinterpret_cast<f2v*>(slot + k * 1024 + lane * 8) = f2v{e[0], e[1]};
-                *reinterpret_cast<f2v*>(slot + k * 1024 + 512 + lane * 8) = f2v{e[2], e[3]};
-            }
-        } else {  // ROW16 slot: lane -> (row lane >> 2, quad lane & 3)
-            f32x4 e;
-#pragma unroll
-            for (int n = 0; n < 4; ++n) {
-                const int col = b * 16 + 4 * (lane & 3) + n;
-                const int k = col / x.C, c = col - k * x.C;
-                e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + pc * 16 + (lane >> 2)), c, dummy) : 0.f;
-            }
-            *reinterpret_cast<f32x4*>(slot + lane * 16) = e;
+        for (int n = 0; n < 4; ++n) {
+            const int col = b * 16 + 4 * (lane & 3) + n;
+            const int k = col / x.C, c = col - k * x.C;
+            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + pc * 16 + (lane >> 2)), c, x.A) : 0.f;
         }
+        *reinterpret_cast<f32x4*>(raw + pc * 1024 + lane * 16) = e;
     }
     return 0;
 }
 
-// s_waitcnt vmcnt(n) for a runtime n (the loader's DMAs of the stage just issued).
+// s_waitcnt vmcnt(n) for a runtime n (the loader's DMAs just issued stay in flight).
 __device__ __forceinline__ void hxsWaitVm(int n) {
 #define GAR_VM(v) case v: __builtin_amdgcn_s_waitcnt(((v) & 15) | (((v) >> 4) << 14) | 0x0F70); break;
     switch (n) {
@@ -274,8 +316,7 @@ __device__ __forceinline__ void hxsWaitVm(int n) {
 #undef GAR_VM
 }
 
-// Loader: one item's 4 values (row `row` of the stage, quad q) -> ring rows
-// (hi/lo split, mirror, loud marking).
+// One item (row `row` of the stage, quad q) -> ring rows (hi/lo split, mirror, loud marking).
 __device__ __forceinline__ void hxsPutItem(const HxsArgs& x, const HxsStage& st, int p0, int q, int row, f32x4 e,
                                            char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
     const int t = st.T0 + row;  // column-relative row
@@ -302,46 +343,40 @@ __device__ __forceinline__ void hxsPutItem(const HxsArgs& x, const HxsStage& st,
     }
 }
 
-// Loader: this wave's slots of a stage -> ring.
-__device__ __forceinline__ void hxsConvert(const HxsArgs& x, const HxsStage& st, int wl, int lane, const char* slots,
+// Every wave: its share of a staged raw buffer -> ring.  Items are (quad, row)
+// with rows padded to 64 so a wave instruction covers 64 consecutive rows of
+// one quad (conflict-free raw reads and ring writes); thread t of nth takes
+// items t, t + nth, ...
+__device__ __forceinline__ void hxsConvert(const HxsArgs& x, const HxsStage& st, const char* raw, int tid, int nth,
                                            char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
-    const int RPc = hxsPieceRows(x);
-    const int npc = (st.nrow + RPc - 1) / RPc;
+    const int pad = (st.nrow + 63) & ~63;
     const int p0 = uni(st.T0 % x.R);  // ring row of the stage's first row
-    for (int pc = wl, s = 0; pc < npc; pc += kHxsLoaders, ++s) {
-        const char* slot = slots + s * x.pieceBytes;
-        if (x.fmt == 1) {
+    // two items per pass: their raw reads are in flight together
+    for (int j0 = 0; j0 < kHxsConvMax; j0 += 2) {
+        if (j0 * nth >= 4 * pad) break;  // uniform
+        f32x4 e[2];
+        int q[2], row[2];
+        bool ok[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int r = h * 64 + lane, row = pc * 128 + r;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f2v a = *reinterpret_cast<const f2v*>(slot + (2 * q) * 1024 + r * 8);
-                    const f2v c = *reinterpret_cast<const f2v*>(slot + (2 * q + 1) * 1024 + r * 8);
-                    if (row < st.nrow) hxsPutItem(x, st, p0, q, row, f32x4{a.x, a.y, c.x, c.y}, ring, QS, loudLo, loudHi, flag);
-                }
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + (j0 + u) * nth;
+            q[u] = (i >= pad) + (i >= 2 * pad) + (i >= 3 * pad);
+            row[u] = i - q[u] * pad;
+            ok[u] = q[u] <= 3 && row[u] < st.nrow;
+            const int qq = ok[u] ? q[u] : 0, rr = ok[u] ? row[u] : 0;
+            if (x.fmt == 1) {
+                const char* sp = raw + (rr >> 7) * 8192 + (rr & 127) * 8 + (2 * qq) * 1024;
+                const f2v a = *reinterpret_cast<const f2v*>(sp);
+                const f2v c = *reinterpret_cast<const f2v*>(sp + 1024);
+                e[u] = f32x4{a.x, a.y, c.x, c.y};
+            } else {
+                e[u] = *reinterpret_cast<const f32x4*>(raw + (rr >> 4) * 1024 + (rr & 15) * 64 + qq * 16);
             }
-        } else {
-            const int row = pc * 16 + (lane >> 2), q = lane & 3;
-            const f32x4 e = *reinterpret_cast<const f32x4*>(slot + lane * 16);
-            if (row < st.nrow) hxsPutItem(x, st, p0, q, row, e, ring, QS, loudLo, loudHi, flag);
         }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (ok[u]) hxsPutItem(x, st, p0, q[u], row[u], e[u], ring, QS, loudLo, loudHi, flag);
     }
-}
-
-// Stage k of a block: k = 0 rows [0, Wg), k >= 1 rows [Wg + (k-1)*G*Qc, Wg + k*G*Qc).
-__device__ __forceinline__ HxsStage hxsStage(const HxsArgs& x, int b, int T0, int nrow) {
-    HxsStage s;
-    s.T0 = T0;
-    s.nrow = nrow;
-    const int c0 = b * 16, c1 = c0 + 15;
-    const int64_t kmin = c0 / x.C;
-    // rows past the raw input read zeros through the buffer records (hxsRsrc);
-    // rows before it (history, stream start), partial blocks and layouts
-    // without an LDS-DMA form are gathered
-    const int64_t tlo = (x.a_lo + kmin * x.Np) * x.Qc + T0;
-    s.fast = (x.fmt == 1 || (x.fmt == 2 && x.C % 16 == 0)) && c1 < x.ncols && tlo >= x.fastLo && x.fastHi > x.fastLo;
-    return s;
 }
 
 template <int VST>
@@ -366,19 +401,32 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
     }
 }
 
-// Compute waves (one row block each).  The barrier sequence per block --
-// reset, prologue, one per group, [fixup] -- matches hxsLoaders exactly: the
-// two roles run in separate loops so their registers (A vs raw rows) never
-// live at the same time.
+// The per-block protocol shared by both roles (identical barrier sequences).
+// Loads j = 0 .. P + ngroups - 2 (hxsLoad) go through raw buffer j % 3:
+//   reset B | loaders issue loads 0, 1, wait load 0 B |
+//   step j = 0 .. P + ngroups - 1: every wave converts load j; loaders issue
+//   load j + 2 and wait load j + 1; compute waves run MFMA group j - P (when
+//   >= 0: stage 0 and stages 1 .. j - P are in the ring); B | [fixup]
+struct HxsShared {
+    char* ring;
+    uint32_t QS;
+    int* loudLo;
+    int* loudHi;
+    int* flag;
+    char* raw;  // [3][stageBytes]
+};
+
+// Compute waves (one row block each).
 template <int NS, int VST>
-__device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_t QS, const int* loudLo, const int* loudHi,
-                                           const int* flag, int wt, int lane) {
+__device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh_, int wt, int lane) {
+    const uint32_t QS = sh_.QS;
     const int sh = -(x.ea + kHxXs);
     const int GQ = x.G * x.Qc;
     const int grp = lane >> 4, l16 = lane & 15;
     const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
     const int* pt = x.progs + kBgProgInts * wt;
     const int u0 = uni(pt[4]), rbw = uni(pt[3]);
+    const int tid = wt * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
     h8v Ah[NS], Al[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -389,11 +437,13 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
     const uint32_t pstep = 8u * static_cast<uint32_t>(x.Qc);
     const int nslot = x.R / GQ;
-    unsigned long long tm = 0, tw = 0;
+    unsigned long long tm = 0, tw = 0, tcv = 0;
+
+    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
 
     for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
         hxsBarrier();  // loud state reset; the previous block's ring reads done
-        hxsBarrier();  // prologue staged
+        hxsBarrier();  // load 0 landed
         const int col = b * 16 + l16;
         const bool colOk = col < x.ncols;
         const int kcol = col / x.C, ccol = col - kcol * x.C;
@@ -402,11 +452,11 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_
         // output of relative period p: whole-quad store, or checked elements at the launch edges
         auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
             const f32x4 y = hxScale(oA, oL, sh);
-            if (x.dbg & 8) return;
             const int64_t a = aCol + p;
             const int64_t o0 = a * x.Pc + oRow0;
             const bool live = colOk && p < x.Np && a < x.a_hi;
-            if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+            if (x.dbg & 2) {
+            } else if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
                 char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
                 hxsStoreFast<VST>(x, pp, y, lane);
             } else if (live) {
@@ -421,10 +471,20 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_
                 }
             }
         };
-        for (int g = 0; g < x.ngroups; ++g) {
+        for (int j = 0; j < P + x.ngroups; ++j) {
+            // load j -> ring (this wave's share), then the MFMA periods of group j - P
             const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            if (j < nL && !((x.dbg & 16) && j >= P) && !((x.dbg & 32) && j >= P))
+                hxsConvert(x, hxsLoad(x, b, j, P), sh_.raw + (j % 3) * x.stageBytes, tid, nth, sh_.ring, QS,
+                           sh_.loudLo, sh_.loudHi, sh_.flag);
+            if (x.prof) tcv += __builtin_amdgcn_s_memtime() - t0;
+            const int g = j - P;
+            if (g < 0) {
+                hxsBarrier();
+                continue;
+            }
             const int slot = g % nslot;
-            uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) +
+            uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(sh_.ring + laneOff))) +
                           8u * static_cast<uint32_t>(slot * GQ + u0);
             h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
             // one period's MFMA program into nA (hi-x products) and nL (lo-x products); the
@@ -454,8 +514,12 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_
                 aH = aN;
             };
             const int p0 = g * x.G;
-            if (x.dbg & 4) { hxsBarrier(); continue; }
             f32x4 a0, a1 = {0, 0, 0, 0}, l0, l1 = a1;
+            if (x.dbg & 4) {
+                epilogue(a1, l1, p0);
+                if (x.G > 1) epilogue(a1, l1, p0 + 1);
+                if (x.G > 2) epilogue(a1, l1, p0 + 2);
+            } else {
             // periods in pairs (alternating accumulators): period i's stores issue from
             // inside period i+1's MFMA stream
             period(a0, l0, a1, l1, false, 0, x.G == 1);
@@ -470,86 +534,87 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, char* ring, uint32_
             } else {
                 epilogue(a0, l0, p0 + i - 1);
             }
+            }
             const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            hxsBarrier();  // group done; stage g+1 staged
+            hxsBarrier();  // step done: load j in the ring, load j + 1 landed
             if (x.prof) { tm += t1 - t0; tw += __builtin_amdgcn_s_memtime() - t1; }
         }
-        if (*flag) {
+        if (*sh_.flag) {  // uniform (LDS after the barrier)
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
             __syncthreads();
-            hxsFixup(hxsCold(), b, loudLo, loudHi);
+            hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
         }
     }
     if (x.prof && lane == 0) {
         atomicAdd(x.prof + 4, tm);
         atomicAdd(x.prof + 5, tw);
         atomicAdd(x.prof + 6, 1ull);
+        atomicAdd(x.prof + 15, tcv);
     }
 }
 
-// Loader waves: stage 0 before the first group; during group g the DMAs of
-// stage g+2 are issued first, then the wave waits for its own DMAs of stage
-// g+1 (issued a group earlier) and converts them into the ring.
-__device__ __forceinline__ void hxsLoaders(const HxsArgs& x, char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag,
-                                           char* rawAll, int wl, int lane) {
+// Loader waves: the DMAs (or gathers) of every stage, two groups ahead, and their share of the conversion.
+__device__ __forceinline__ void hxsLoaders(const HxsArgs& x, const HxsShared& sh_, int wl, int lane) {
     const int GQ = x.G * x.Qc;
-    char* raw[2] = {rawAll + (2 * wl) * x.slotBytes, rawAll + (2 * wl + 1) * x.slotBytes};
-    unsigned long long tc = 0, tl = 0, tb = 0, tp = 0;
-    const unsigned long long tStart = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+    const int tid = (x.nprog + wl) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
+    unsigned long long tc = 0, tl = 0, tb = 0, ti = 0, tpre = 0, tloop = 0;
     const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
     for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
-        const unsigned long long tp0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-        if (wl == 0 && lane < 16) { loudLo[lane] = INT_MAX; loudHi[lane] = -1; }
-        if (wl == 0 && lane == 0) *flag = 0;
+        if (wl == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
+        if (wl == 0 && lane == 0) *sh_.flag = 0;
         hxsBarrier();  // loud state reset; the previous block's ring reads done
-        for (int T0 = 0; T0 < x.Wg; T0 += GQ) {
-            const HxsStage st = hxsStage(x, b, T0, min(GQ, x.Wg - T0));
-            hxsFetch(x, st, b, wl, lane, raw[0]);
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMAs landed
-            hxsConvert(x, st, wl, lane, raw[0], ring, QS, loudLo, loudHi, flag);
-        }
-        if (x.ngroups > 1) hxsFetch(x, hxsStage(x, b, x.Wg, GQ), b, wl, lane, raw[1]);  // stage 1
-        hxsBarrier();  // prologue staged
-        if (x.prof) tp += __builtin_amdgcn_s_memtime() - tp0;
-        for (int g = 0; g < x.ngroups; ++g) {
+        hxsIssue(x, hxsLoad(x, b, 0, P), b, wl, lane, sh_.raw);
+        hxsWaitVm(nL > 1 ? hxsIssue(x, hxsLoad(x, b, 1, P), b, wl, lane, sh_.raw + x.stageBytes) : 0);
+        hxsBarrier();  // load 0 landed
+        if (x.prof) tpre += __builtin_amdgcn_s_memrealtime() - rStart;
+        for (int j = 0; j < P + x.ngroups; ++j) {
             const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            unsigned long long t1 = t0, t2 = t0;
-            if (g + 1 < x.ngroups) {
-                int nd = 0;
-                if (g + 2 < x.ngroups) nd = hxsFetch(x, hxsStage(x, b, x.Wg + (g + 1) * GQ, GQ), b, wl, lane, raw[g & 1]);
-                if (x.prof) t1 = __builtin_amdgcn_s_memtime();
-                hxsWaitVm(nd);  // stage g+1's DMAs (issued during group g-1) landed
-                hxsConvert(x, hxsStage(x, b, x.Wg + g * GQ, GQ), wl, lane, raw[(g + 1) & 1], ring, QS, loudLo, loudHi, flag);
-                if (x.prof) t2 = __builtin_amdgcn_s_memtime();
-            }
-            hxsBarrier();  // group done; stage g+1 staged
+            const bool solo = (x.dbg & 32) && j >= P;  // loaders convert the whole load
+            if (j < nL && !((x.dbg & 16) && j >= P))
+                hxsConvert(x, hxsLoad(x, b, j, P), sh_.raw + (j % 3) * x.stageBytes, solo ? wl * 64 + lane : tid,
+                           solo ? 64 * kHxsLoaders : nth, sh_.ring, sh_.QS,
+                           sh_.loudLo, sh_.loudHi, sh_.flag);
+            const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            const int nd = (j + 2 < nL && !((x.dbg & 1) && j >= P))
+                               ? hxsIssue(x, hxsLoad(x, b, j + 2, P), b, wl, lane, sh_.raw + ((j + 2) % 3) * x.stageBytes)
+                               : 0;
+            const unsigned long long t1b = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            hxsWaitVm(nd);  // load j + 1 landed
+            const unsigned long long t2 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+            if (x.prof) ti += t1b - t1;
+            hxsBarrier();  // step done
             if (x.prof) {
                 const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-                tl += t1 - t0; tc += t2 - t1; tb += t3 - t2;
+                tc += t1 - t0; tl += t2 - t1; tb += t3 - t2;
             }
         }
-        if (*flag) {
+        if (x.prof) tloop = __builtin_amdgcn_s_memrealtime();
+        if (*sh_.flag) {
             __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
-            hxsFixup(hxsCold(), b, loudLo, loudHi);
+            hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
         }
     }
     if (x.prof && lane == 0) {
         const unsigned long long rEnd = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(x.prof + 8, tpre);
+        atomicAdd(x.prof + 12, rEnd - tloop);
         atomicAdd(x.prof + 0, tc);
         atomicAdd(x.prof + 1, tl);
         atomicAdd(x.prof + 2, tb);
         atomicAdd(x.prof + 3, 1ull);
-        atomicAdd(x.prof + 7, tp);
-        atomicAdd(x.prof + 8, __builtin_amdgcn_s_memtime() - tStart);
+        atomicAdd(x.prof + 7, ti);
         atomicAdd(x.prof + 9, rEnd - rStart);
+        if (wl == 0 && blockIdx.x < 4096) {  // per-workgroup start / life of the last launch
+            x.prof[64 + 2 * blockIdx.x] = rStart;
+            x.prof[65 + 2 * blockIdx.x] = rEnd - rStart;
+        }
         if (x.nblocks > 16) {
             atomicMin(x.prof + 10, rStart);
             atomicMax(x.prof + 11, rEnd);
-            atomicMax(x.prof + 12, rStart);
             atomicMin(x.prof + 13, rEnd - rStart);
             atomicMax(x.prof + 14, rEnd - rStart);
-            if (wl == 0) atomicAdd(x.prof + 15, (rEnd - rStart) > 20000ull ? 1ull : 0ull);  // WGs above 200 us
         }
     }
 }
@@ -557,19 +622,20 @@ __device__ __forceinline__ void hxsLoaders(const HxsArgs& x, char* ring, uint32_
 template <int NS, int VST>
 __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
-    char* ring = reinterpret_cast<char*>(smem);
-    int* loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(QS));
-    int* loudHi = loudLo + 16;
-    int* flag = loudHi + 16;
-    char* rawAll = reinterpret_cast<char*>(smem + 4 * static_cast<size_t>(QS) + 256);  // [loader][2][slotBytes]
+    HxsShared s;
+    s.QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
+    s.ring = reinterpret_cast<char*>(smem);
+    s.loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(s.QS));
+    s.loudHi = s.loudLo + 16;
+    s.flag = s.loudHi + 16;
+    s.raw = reinterpret_cast<char*>(smem + 4 * static_cast<size_t>(s.QS) + 256);
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
-    if (wt < x.nprog) hxsCompute<NS, VST>(x, ring, QS, loudLo, loudHi, flag, wt, lane);
-    else hxsLoaders(x, ring, QS, loudLo, loudHi, flag, rawAll, wt - x.nprog, lane);
+    if (wt < x.nprog) hxsCompute<NS, VST>(x, s, wt, lane);
+    else hxsLoaders(x, s, wt - x.nprog, lane);
 }
 
-// Launch (explicitly instantiated in gar_hxs.hip).
+// Launch (explicitly instantiated in gar_hxs_i*.hip).
 template <int NS, int VST>
 hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
     setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>));
