@@ -1,24 +1,38 @@
 #!/usr/bin/env python3
 """bench.py -- BASELINE.json metric on MI355X.
 
-Metric: Msamples/s resampled (float32, 44.1k->48k QualityHigh) + RMS error vs
-the reference (oracle).  Workload (BASELINE configs[1]): one stereo float32
-stream of 600 s (26,460,000 frames) per GPU, 44.1 kHz -> 48 kHz through
-resampler.New with QualityHigh (engine.Quality24Bit), inputs resident in HBM.
-One step = Reset + Process(whole stream) + Flush, i.e. the complete job; the
-ProcessInto chunking of the reference does not change any output value
-(constant.go:270-276), so the stream goes through in one call.
+Metric: Msamples/s resampled (input samples summed over channels per second)
++ RMS error vs the reference (oracle/).  Default workload (BASELINE configs[1],
+SURVEY.md 8(d) config 2): one stereo float32 stream of 600 s (26,460,000
+frames) per GPU, 44.1 kHz -> 48 kHz through resampler.New with QualityHigh
+(engine.Quality24Bit), inputs resident in HBM.  One step = Reset + Process
+(whole stream, one device call) + Flush, i.e. the complete job; ProcessInto
+chunking does not change any output value (constant.go:270-276, checked
+bit for bit by tests/test_gpu_parity.py), and the chunked drop-in usage is
+timed beside it (`streaming`).
 
-N>1 GPUs: one process per GPU (torchrun), every rank resamples its own
-independent stereo stream (weak scaling, streams sharded, no data-path
-collective); RCCL (torch.distributed nccl) only all-reduces the timing and
-sample counters after the timed region.  value = all input samples of all
-ranks / max-over-ranks wall time.
+Other workloads (--workload):
+  ns256  north_star: 256 ch f32 44.1k->48k QualityHigh, 60 s per GPU
+  cfg3   256 ch f32 48k->44.1k QualityVeryHigh, 10 s per GPU
+  cfg4   1024 independent stereo streams x 10 s, 44.1k->48k QualityHigh,
+         sharded contiguously over the ranks (one NewBatch per rank; total
+         work fixed: strong scaling)
+  cfg5   8 ch f64 96k->44.1k QualityVeryHigh, 60 s in 4800-frame ProcessInto
+         chunks (decimator -> DFTx2 -> polyphase, f64 compute)
+
+N>1 GPUs: one process per GPU (torchrun), no data-path collective; RCCL
+(torch.distributed nccl) only reduces the timing and sample counters after
+the timed region.  value = all input samples of all ranks / max-over-ranks
+wall time.
 """
 import argparse
 import json
 import os
+import signal as _signal
+import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -26,17 +40,48 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "go-audio-resampler_amd")]
 
 import numpy as np  # noqa: E402
 
-METRIC = "Msamples/s resampled (float32, 44.1k→48k QualityHigh) + RMS error vs Go ref"
-IN_RATE, OUT_RATE, CHANNELS = 44100, 48000, 2
-# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level table)
-PEAK_F32_MATRIX_TFLOPS = 157.3
-PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
+BASELINE_METRIC = "Msamples/s resampled (float32, 44.1k→48k QualityHigh) + RMS error vs Go ref"
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md chip table; f64 from SURVEY.md 8(d))
 PEAK_HBM_GBPS = 8000.0
-# reference-algorithm flops per input sample (cfg2)
-REF_ALGO_FLOPS_PER_SAMPLE = 1017.6
+PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
+PEAK_F64_MATRIX_TFLOPS = 78.6
+# reference-algorithm flops per input sample
+REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6}
+DECIM_MACS_PER_INPUT = 611.5  # cfg5 stage 1: factor 2, 1223 taps
+# New path: preset -> precision -> engine quality (stages.go:54-70, pipeline_builder.go:76-100)
+ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit}
+
+WORKLOADS = {
+    "cfg2": dict(name="cfg2_stereo_f32_44k1_48k_q24_600s", ir=44100, orr=48000, ch=2, preset="High", seconds=600.0,
+                 io="f32", compute="F32", streams=1, scaling="weak", chunk=0,
+                 desc="BASELINE configs[1]: stereo float32 44.1k->48k QualityHigh (engine Quality24Bit), 600 s "
+                      "stream per GPU, HBM-resident, one Process+Flush per step"),
+    "ns256": dict(name="ns256_256ch_f32_44k1_48k_q24_60s", ir=44100, orr=48000, ch=256, preset="High", seconds=60.0,
+                  io="f32", compute="F32", streams=1, scaling="weak", chunk=0,
+                  desc="north_star: 256-channel float32 44.1k->48k QualityHigh, 60 s per GPU, one Process+Flush"),
+    "cfg3": dict(name="cfg3_256ch_f32_48k_44k1_q32_10s", ir=48000, orr=44100, ch=256, preset="VeryHigh", seconds=10.0,
+                 io="f32", compute="F32", streams=1, scaling="weak", chunk=0,
+                 desc="BASELINE configs[2]: 256-channel float32 48k->44.1k QualityVeryHigh (Quality32Bit), 10 s"),
+    "cfg4": dict(name="cfg4_1024x_stereo_f32_44k1_48k_q24_10s", ir=44100, orr=48000, ch=2, preset="High",
+                 seconds=10.0, io="f32", compute="F32", streams=1024, scaling="strong", chunk=0,
+                 desc="BASELINE configs[3]: 1024 independent stereo float32 streams x 10 s 44.1k->48k QualityHigh, "
+                      "sharded contiguously over the ranks, one NewBatch per rank"),
+    "cfg5": dict(name="cfg5_8ch_f64_96k_44k1_q32_60s_4800chunks", ir=96000, orr=44100, ch=8, preset="VeryHigh",
+                 seconds=60.0, io="f64", compute="F64", streams=1, scaling="weak", chunk=4800,
+                 desc="BASELINE configs[4]: 8-channel float64 96k->44.1k QualityVeryHigh multi-stage pipeline "
+                      "(decimator x1/2 -> DFT x2 -> polyphase), 60 s streamed in 4800-frame ProcessInto chunks"),
+}
 
 
-def synth_stream(frames, channels, seed, rate=IN_RATE):
+def metric_for(key, w):
+    if key == "cfg2":
+        return BASELINE_METRIC
+    io = "float32" if w["io"] == "f32" else "float64"
+    return (f"Msamples/s resampled ({io}, {w['ir'] / 1000:g}k→{w['orr'] / 1000:g}k Quality{w['preset']}, "
+            f"{w['ch'] * w['streams']} ch) + RMS error vs Go ref")
+
+
+def synth_stream(frames, channels, seed, rate):
     """0.7 sin(440 Hz) + 0.2 sin(1750 Hz) + 0.1 (U - 0.5) per channel
     (the generator shape of processinto_test.go:19-30), float32 [frames, ch]."""
     out = np.empty((frames, channels), dtype=np.float32)
@@ -47,6 +92,21 @@ def synth_stream(frames, channels, seed, rate=IN_RATE):
         out[:, c] = (0.7 * np.sin(2 * np.pi * 440 * t + p1) + 0.2 * np.sin(2 * np.pi * 1750 * t + p2)
                      + 0.1 * (rng.random(frames) - 0.5))
     return out
+
+
+def synth_device(torch, frames, channels, seed, rate, dtype):
+    """The same signal shape generated on the device (10^9 samples in well under a second)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    t = torch.arange(frames, device="cuda", dtype=torch.float64) / rate
+    ph = torch.rand((2, channels), generator=g, device="cuda", dtype=torch.float64) * 2 * np.pi
+    x = torch.empty((frames, channels), device="cuda", dtype=dtype)
+    blk = max(1, (1 << 26) // max(channels, 1))
+    for s in range(0, frames, blk):
+        tt = t[s:s + blk, None]
+        noise = torch.rand((tt.shape[0], channels), generator=g, device="cuda", dtype=torch.float64) - 0.5
+        x[s:s + blk] = (0.7 * torch.sin(2 * np.pi * 440 * tt + ph[0]) + 0.2 * torch.sin(2 * np.pi * 1750 * tt + ph[1])
+                        + 0.1 * noise).to(dtype)
+    return x
 
 
 def dist_env():
@@ -76,45 +136,131 @@ def reduce_stats(elapsed_s, samples, device=None):
     return float(t.item()), float(s.item())
 
 
-def cpu_baseline(target_s=12.0):
-    """The CPU restatement of the reference path (oracle/, 'port') timed on one
-    host core: New(44.1k->48k, stereo, QualityHigh) Process+Flush in float64
-    (the reference's ProcessFloat32 computes in float64, constant.go:121-146)."""
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count(), avail
+
+
+def cpu_baseline(w, target_s=10.0):
+    """The CPU restatement of the reference path (oracle/, 'port', AVX2 build) timed on
+    the host: New(ir->orr, QualityX) Process+Flush per channel in float64 (the
+    reference's ProcessFloat32 computes in float64, constant.go:121-146), the
+    methodology of throughput_comparison_test.go:102-148.  One core, then every
+    core this process may use (one independent stream per thread, like
+    EnableParallel's goroutine per channel, constant.go:223-249; the oracle
+    releases the GIL inside its C calls)."""
     from oracle import oracle as O
     O.build()
-    probe = 2.0
-    frames = int(probe * IN_RATE)
-    x = synth_stream(frames, CHANNELS, 4242).astype(np.float64)
+    preset = getattr(O, "P_" + w["preset"].upper())
+    ch = min(w["ch"], 2)
 
     def run(xx):
-        r = O.NewResampler(IN_RATE, OUT_RATE, CHANNELS, O.P_HIGH)
+        r = O.NewResampler(w["ir"], w["orr"], ch, preset)
         t0 = time.perf_counter()
-        for c in range(CHANNELS):
+        for c in range(ch):
             r.process(xx[:, c], c)
             r.flush(c)
         return time.perf_counter() - t0
 
+    probe = 1.0
+    x = synth_stream(int(probe * w["ir"]), ch, 4242, w["ir"]).astype(np.float64)
     dt = run(x)
-    secs = max(probe, min(600.0, probe * target_s / max(dt, 1e-3)))
-    frames = int(secs * IN_RATE)
-    x = synth_stream(frames, CHANNELS, 4242).astype(np.float64)
-    dt = run(x)
-    return {"value": round(frames * CHANNELS / dt / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{secs:.1f} s of stereo 44.1k->48k QualityHigh (New path, float64 compute), "
-                      f"Process+Flush, single thread, {dt:.1f} s wall"}
+    secs = max(probe, min(w["seconds"], probe * target_s / max(dt, 1e-3)))
+    frames = int(secs * w["ir"])
+    x = synth_stream(frames, ch, 4242, w["ir"]).astype(np.float64)
+    dt1 = run(x)
+    one = frames * ch / dt1 / 1e6
+    model, ncpu, avail = cpu_info()
+    threads = max(1, min(avail, 16))  # the GPU box's CPU share per GPU is 16
+    secs_t = max(probe, secs / 2)
+    fr_t = int(secs_t * w["ir"])
+    xt = x[:fr_t]
+    res = [0.0] * threads
+
+    def worker(i):
+        res[i] = run(xt)
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dtn = time.perf_counter() - t0
+    alln = threads * fr_t * ch / dtn / 1e6
+    return {"value": round(one, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": f"{secs:.1f} s of {ch}-ch {w['ir']}->{w['orr']} Quality{w['preset']} (New path, float64 "
+                      f"compute, oracle/ AVX2 build), Process+Flush, single thread, {dt1:.1f} s wall",
+            "all_cores": {"value": round(alln, 3), "cores": threads,
+                          "sample": f"{threads} threads x {secs_t:.1f} s independent {ch}-ch streams, "
+                                    f"{dtn:.1f} s wall"},
+            "cpu_model": model, "nproc": ncpu, "cpus_usable": avail}
 
 
-def load_traffic(workload):
-    """HBM bytes per launch of the dominant kernel from the committed PMC run
-    (profiles/pmc_<workload>.json written by tools/pmc_traffic.py), else None."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if not os.path.exists(p):
-        return None
-    try:
-        with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+def pmc_traffic(args, kernel_keys):
+    """HBM bytes per launch of the dominant kernel, measured now: two rocprofv3 PMC
+    passes (FETCH_SIZE, then WRITE_SIZE: 3 + 2 TCC counters do not fit one pass)
+    over a short child run of this same workload; corrected as
+    MI355X_MICROARCH.md's HBM section prescribes (KiB; gfx950 FETCH_SIZE counts
+    half the bytes of a wide streaming read -> x2).  None if the profiler is
+    unavailable or fails."""
+    import csv
+    import glob
+    prof = "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    out = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="gar_pmc_", dir="/tmp")
+        cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.join(ROOT, "bench.py"), "--workload", args.workload, "--steps", "2",
+               "--warmup", "1", "--no-cpu-baseline", "--check-seconds", "0", "--no-pmc", "--no-streaming"]
+        try:
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                 start_new_session=True)
+            try:
+                p.wait(timeout=180)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, _signal.SIGKILL)
+                p.wait()
+                return None, f"{counter} pass timed out"
+            if p.returncode != 0:
+                return None, f"{counter} pass rc {p.returncode}"
+        except OSError as e:
+            return None, str(e)
+        per, grid = {}, {}
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    name = row.get("Kernel_Name", "")
+                    if not any(kk in name for kk in kernel_keys):
+                        continue
+                    key = (f, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                    per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+                    grid[key] = int(float(row.get("Grid_Size") or 0))
+        if not per:
+            return None, f"{counter}: no dispatch of {kernel_keys}"
+        gmax = max(grid.values())
+        vals = [v for k, v in per.items() if grid[k] == gmax]
+        out[counter] = sum(vals) / len(vals)
+    rd = out["FETCH_SIZE"] * 1024 * 2
+    wr = out["WRITE_SIZE"] * 1024
+    return {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}, None
 
 
 def main():
@@ -122,10 +268,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--seconds", type=float, default=600.0, help="stream length per GPU (BASELINE cfg2: 600)")
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--seconds", type=float, default=None, help="stream length override")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check-seconds", type=float, default=5.0, help="prefix checked against the oracle")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live PMC traffic passes")
+    ap.add_argument("--no-streaming", action="store_true", help="skip the chunked drop-in timing")
+    ap.add_argument("--check-seconds", type=float, default=5.0, help="prefix (and suffix) checked against the oracle")
     args = ap.parse_args()
+    w = dict(WORKLOADS[args.workload])
+    if args.seconds:
+        w["seconds"] = args.seconds
 
     import torch
     import gar
@@ -139,76 +291,161 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    frames = int(round(args.seconds * IN_RATE))
-    lo, hi = shard_streams(world, rank, world)  # one stereo stream per rank
-    x_host = synth_stream(frames, CHANNELS, 4242 + 2 * lo)
-    x = torch.from_numpy(x_host).to(dev)
+    frames = int(round(w["seconds"] * w["ir"]))
+    if w["scaling"] == "strong":
+        s_lo, s_hi = shard_streams(w["streams"], rank, world)
+    else:
+        s_lo, s_hi = rank, rank + 1  # one stream (batch) per rank
+    n_streams = s_hi - s_lo
+    C = w["ch"] * (n_streams if w["scaling"] == "strong" else 1)
+    tdt = torch.float32 if w["io"] == "f32" else torch.float64
+    x_host = None
+    if args.workload == "cfg2":  # the exact generator of the round-1 line (numpy, per-channel seeds)
+        x_host = synth_stream(frames, C, 4242 + 2 * s_lo, w["ir"])
+        x = torch.from_numpy(x_host).to(dev)
+    else:
+        x = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], tdt)
 
-    r = gar.New(gar.Config(IN_RATE, OUT_RATE, CHANNELS, gar.QualityHigh, ComputeDtype=gar.F32, Device=dev.index))
-    n_out = gar.lib().gar_device_output_size(r._h, frames)
-    r.Reset()
-    y = torch.empty((n_out, CHANNELS), dtype=torch.float32, device=dev)
-    yf = torch.empty((4096, CHANNELS), dtype=torch.float32, device=dev)
+    cfg = gar.Config(w["ir"], w["orr"], w["ch"], getattr(gar, "Quality" + w["preset"]),
+                     ComputeDtype=getattr(gar, w["compute"]), Device=dev.index)
+    r = gar.NewBatch(cfg, n_streams) if w["scaling"] == "strong" else gar.New(
+        gar.Config(w["ir"], w["orr"], C, getattr(gar, "Quality" + w["preset"]),
+                   ComputeDtype=getattr(gar, w["compute"]), Device=dev.index))
+    chunk = w["chunk"]
+    if chunk:
+        bounds = [(s, min(chunk, frames - s)) for s in range(0, frames, chunk)]
+    else:
+        bounds = [(0, frames)]
+    # output bound: the exact total depends on the carried phase, so allocate ratio*frames + slack
+    n_out = int(frames * w["orr"] / w["ir"]) + 64 * (len(bounds) + 1)
+    y = torch.empty((n_out, C), dtype=tdt, device=dev)
+    yf = torch.empty((max(gar.lib().gar_device_flush_size(r._h), 1) + 4096, C), dtype=tdt, device=dev)
 
     def step():
         r.Reset()
-        r.process_device(x, out=y)
-        return r.flush_device(out=yf)
+        o = 0
+        for s, n in bounds:
+            o += r.process_device(x[s:s + n], out=y[o:]).shape[0]
+        tail = r.flush_device(out=yf)
+        return o, tail.shape[0]
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     r.profile(True)
-    r.profile_read(0)
+    for k in range(4):
+        r.profile_read(k)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        tail = step()
+        n_proc, n_tail = step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    kms, launches = r.profile_read(0)
+    prof = {k: r.profile_read(k) for k in range(4)}
     r.profile(False)
-    n_tail = tail.shape[0]
 
-    local_samples = frames * CHANNELS * args.steps
+    local_samples = frames * C * args.steps
     elapsed, total_samples = reduce_stats(t1 - t0, local_samples, dev)
 
-    # parity of a prefix against the CPU oracle (rank 0)
+    # parity vs the CPU oracle (rank 0): a prefix of the first and last channels, and a
+    # suffix (the last seconds of Process + the whole Flush tail) for single-stage designs
     rms = None
+    rms_tail = None
     if rank == 0 and args.check_seconds > 0:
         from oracle import oracle as O
         O.build()
-        m = int(args.check_seconds * IN_RATE)
-        ref = O.NewResampler(IN_RATE, OUT_RATE, CHANNELS, O.P_HIGH)
-        got = y.cpu().numpy().astype(np.float64)
+        preset = getattr(O, "P_" + w["preset"].upper())
+        m = min(frames, int(args.check_seconds * w["ir"]))
+        got = y[:n_proc].double().cpu().numpy()
+        chans = sorted({0, C - 1})
         errs = []
-        for c in range(CHANNELS):
-            want = ref.process(x_host[:m, c].astype(np.float64), c)
+        for c in chans:
+            xc = (x_host[:m, c] if x_host is not None else x[:m, c].cpu().numpy()).astype(np.float64)
+            ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
+            want = ref.process(xc, 0)
             errs.append(np.mean((got[: len(want), c] - want) ** 2))
         rms = float(np.sqrt(np.mean(errs)))
+        # suffix: a single-stage fused design repeats every Qc inputs / Pc outputs, so the oracle
+        # restarted at input m0 = k*Qc reproduces outputs k*Pc + j once its transient has passed
+        geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), ENGINE_Q[w["preset"]](gar))
+        stages = O.NewResampler(w["ir"], w["orr"], 1, preset).stages()[1]
+        if len(stages) == 1 and geom.fused:
+            Qc, Pc = geom.fir_period_in, geom.fir_period_out
+            k = max(0, (frames - m) // Qc)
+            m0 = k * Qc
+            skip = 4 * geom.fir_taps_max
+            tail = yf[:n_tail].double().cpu().numpy()
+            errs = []
+            for c in chans:
+                xc = (x_host[m0:, c] if x_host is not None else x[m0:, c].cpu().numpy()).astype(np.float64)
+                ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
+                want = np.concatenate([ref.process(xc, 0), ref.flush(0)])
+                full = np.concatenate([got[k * Pc:, c], tail[:, c]])
+                if len(full) != len(want):
+                    errs.append(float("inf"))
+                    continue
+                errs.append(np.mean((full[skip:] - want[skip:]) ** 2))
+            rms_tail = float(np.sqrt(np.mean(errs)))
 
-    # roofline of the dominant kernel: the fused DFTx2->polyphase FIR launch of
-    # Process (HIP events on the launch stream, inside the library).  The
-    # split-f16 kernel (GAR_F32) needs 2*3*MACs of f16 MFMA work per output
-    # (40 us at the 2.5 PF dense f16 peak for this workload) and moves the
-    # algorithmic bytes once (55 us at 8 TB/s): HBM is the binding roofline.
-    geom, _ = gar.design_engine(48000.0, 48000.0 * (OUT_RATE / IN_RATE), gar.Engine24Bit)
-    useful_macs = geom.useful_macs_per_output
-    outs_per_launch = n_out * CHANNELS
+    # roofline of the dominant kernel (HIP events on the launch stream, inside the library)
+    kinds = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)"}
+    dom = max((0, 1, 2), key=lambda k: prof[k][0])
+    kms, launches = prof[dom]
     launch_s = (kms / 1e3) / max(launches, 1)
-    workload = "cfg2_stereo_f32_44k1_48k_q24_600s"
-    traffic = load_traffic(workload)
-    algo_bytes = frames * CHANNELS * 4 + outs_per_launch * 4
-    achieved_gbps = algo_bytes / launch_s / 1e9 if launches else None
-    split = os.environ.get("GAR_HX", "1") != "0"
-    f16_flops = 2.0 * 3 * useful_macs * outs_per_launch  # three f16 products per useful MAC
-    f32_flops = 2.0 * useful_macs * outs_per_launch
+    in_bytes = 4 if w["io"] == "f32" else 8
+    out_samples_step = (n_proc + n_tail) * C
+    if w["compute"] == "F32":
+        # HBM-bound streaming FIR: algorithmic bytes = input read once + output written once
+        algo_bytes = frames * C * in_bytes + n_proc * C * in_bytes
+        algo_per_launch = algo_bytes / max(launches / args.steps, 1)
+        achieved = algo_per_launch / launch_s / 1e9 if launches else None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
+        kernel_keys = ["hxs_kernel", "hx_kernel"]
+        kname = ("hxs_kernel / hx_kernel (fused DFTx2->polyphase banded FIR, f16-split "
+                 "v_mfma_f32_16x16x32_f16, f32 accumulation)")
+        algo_unit_bytes = algo_per_launch
+    else:
+        # f64: MFMA-bound (f64 matrix rate); useful flops of the dominant stage
+        if dom == 2:
+            flops_step = 2.0 * DECIM_MACS_PER_INPUT * frames * C
+        else:
+            geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), ENGINE_Q[w["preset"]](gar))
+            flops_step = 2.0 * geom.useful_macs_per_output * out_samples_step
+        fl_launch = flops_step / max(launches / args.steps, 1)
+        achieved = fl_launch / launch_s / 1e12 if launches else None
+        roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
+                "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
+        kernel_keys = ["bg_kernel"]
+        kname = f"bg_kernel<double> ({kinds[dom]}, v_mfma_f64_16x16x4_f64)"
+        algo_unit_bytes = None
+    roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[args.workload]
+    roof.update({"traffic": None, "kernel": kname, "kernel_kind": kinds[dom],
+                 "kernel_ms_per_launch": round(launch_s * 1e3, 5), "launches": launches})
+    if algo_unit_bytes:
+        roof["algo_hbm_bytes_per_launch"] = int(algo_unit_bytes)
+        roof["algo_bytes_per_input_sample"] = round(algo_unit_bytes * launches / args.steps / (frames * C), 3)
+    if args.workload in ("cfg2", "ns256", "cfg4"):
+        geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), gar.Engine24Bit)
+        useful = geom.useful_macs_per_output
+        roof["useful_macs_per_output"] = round(useful, 2)
+        outs_launch = n_proc * C / max(launches / args.steps, 1)
+        roof["mfma_tflops_f16"] = round(2.0 * 3 * useful * outs_launch / launch_s / 1e12, 2) if launches else None
+        roof["mfma_peak_tflops_f16"] = PEAK_F16_MATRIX_TFLOPS
+
+    # streaming drop-in usage (rank 0): 4096-frame (cfg5: 4800) chunks through the device
+    # API and through the host C-ABI (ProcessMulti over planar float64, the cgo shim's call)
+    streaming = None
+    if rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak":
+        streaming = time_streaming(gar, torch, w, x, C, dev)
+
     line = {
-        "metric": METRIC,
+        "metric": metric_for(args.workload, w),
         "value": round(total_samples / elapsed / 1e6, 2),
         "unit": "Msamples/s",
         "n_gpus": world,
@@ -216,51 +453,117 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": w["scaling"],
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": w["io"],
         "data": "synthetic",
         "rms_vs_oracle": rms,
+        "rms_vs_oracle_tail": rms_tail,
         "config": {
-            "workload": workload,
-            "description": "BASELINE configs[1]: stereo float32 44.1k->48k QualityHigh (engine Quality24Bit), "
-                           "600 s stream per GPU, HBM-resident, one Process+Flush per step",
-            "channels": CHANNELS,
+            "workload": w["name"],
+            "description": w["desc"],
+            "channels": C,
             "frames_per_stream": frames,
-            "output_frames_per_stream": n_out + n_tail,
-            "streams_per_gpu": 1,
-            "parallelism": f"independent streams, 1 per GPU x {world}",
+            "output_frames_per_stream": n_proc + n_tail,
+            "streams_per_gpu": n_streams,
+            "chunk_frames": chunk or None,
+            "parallelism": (f"{w['streams']} streams sharded over {world} GPUs" if w["scaling"] == "strong"
+                            else f"independent streams, 1 per GPU x {world}"),
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved_gbps, 1) if achieved_gbps else None,
-            "peak": PEAK_HBM_GBPS,
-            "unit": "GB/s",
-            "frac": round(achieved_gbps / PEAK_HBM_GBPS, 4) if achieved_gbps else None,
-            "traffic": traffic,
-            "kernel": ("hx_kernel (fused DFTx2->polyphase banded FIR, f16-split v_mfma_f32_16x16x32_f16, f32 accumulation)"
-                       if split else "bg_kernel<float> (exact-f32 v_mfma_f32_16x16x4_f32)"),
-            "kernel_ms_per_launch": round(launch_s * 1e3, 4),
-            "launches": launches,
-            "algo_hbm_bytes_per_launch": algo_bytes,
-            "algo_bytes_per_input_sample": round(algo_bytes / (frames * CHANNELS), 3),
-            "useful_macs_per_output": round(useful_macs, 2),
-            "mfma_tflops": round((f16_flops if split else f32_flops) / launch_s / 1e12, 2) if launches else None,
-            "mfma_peak_tflops": PEAK_F16_MATRIX_TFLOPS if split else PEAK_F32_MATRIX_TFLOPS,
-            "ref_algo_flops_per_input_sample": REF_ALGO_FLOPS_PER_SAMPLE,
-            "ref_equiv_tflops": round(REF_ALGO_FLOPS_PER_SAMPLE * frames * CHANNELS / launch_s / 1e12, 3)
-            if launches else None,
-        },
+        "roofline": roof,
         "arith": ("f32 I/O; products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
-                  "(error at the level of exact-f32 arithmetic: rms_vs_oracle)" if split else "exact f32 MFMA"),
+                  "(error at the level of exact-f32 arithmetic: rms_vs_oracle)" if w["compute"] == "F32"
+                  else "f64 I/O and f64 MFMA (v_mfma_f64_16x16x4_f64)"),
+        "streaming": streaming,
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_pmc:
+        traffic, err = pmc_traffic(args, kernel_keys)
+        if traffic:
+            per_launch = traffic["bytes"]
+            line["roofline"]["traffic"] = per_launch
+            line["roofline"]["traffic_read"] = traffic["read_bytes"]
+            line["roofline"]["traffic_write"] = traffic["write_bytes"]
+        else:
+            line["roofline"]["traffic_error"] = err
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+        line["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def time_streaming(gar, torch, w, x, C, dev, seconds=60.0):
+    """The reference's own usage pattern (processinto_bench_test.go:12-205): a stream fed in
+    4096-frame ProcessInto calls.  Device API: x already in HBM, one gar_process_device per
+    chunk (asynchronous; one synchronise at the end).  Host C-ABI: planar float64 host
+    buffers, one gar_process_multi_f64 per chunk (what the cgo shim does: H2D, launches,
+    D2H, synchronise inside every call).  Bounded samples of the workload's stream."""
+    import ctypes as Ct
+    chunk = 4096
+    frames = min(x.shape[0], int(seconds * w["ir"]))
+    r = gar.New(gar.Config(w["ir"], w["orr"], C, getattr(gar, "Quality" + w["preset"]), ComputeDtype=gar.F32,
+                           Device=dev.index))
+    y = torch.empty((int(frames * w["orr"] / w["ir"]) + 64 * (frames // chunk + 2), C), dtype=torch.float32,
+                    device=dev)
+    xs = x[:frames]
+
+    def dev_pass():
+        r.Reset()
+        o = 0
+        for s in range(0, frames, chunk):
+            o += r.process_device(xs[s:s + chunk], out=y[o:]).shape[0]
+        r.flush_device()
+        return o
+
+    dev_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev_pass()
+    torch.cuda.synchronize()
+    dt_dev = time.perf_counter() - t0
+    ncalls = (frames + chunk - 1) // chunk
+
+    # host C-ABI: bounded to `hs` seconds (each call round-trips through PCIe)
+    hs = min(seconds / 4, frames / w["ir"])
+    hframes = int(hs * w["ir"])
+    xh = [np.ascontiguousarray(xs[:hframes, c].double().cpu().numpy()) for c in range(C)]
+    rh = gar.New(gar.Config(w["ir"], w["orr"], C, getattr(gar, "Quality" + w["preset"]), ComputeDtype=gar.F32,
+                            Device=dev.index))
+    cap = int(chunk * w["orr"] / w["ir"]) + 64
+    outs = [np.empty(cap) for _ in range(C)]
+    outp = (Ct.c_void_p * C)(*[o.ctypes.data for o in outs])
+    counts = np.zeros(C, dtype=np.int64)
+    L = gar.lib()
+    calls = []
+    for s in range(0, hframes, chunk):
+        n = min(chunk, hframes - s)
+        calls.append(((Ct.c_void_p * C)(*[a.ctypes.data + 8 * s for a in xh]), n))
+
+    def host_pass():
+        rh.Reset()
+        for inp, n in calls:
+            st = L.gar_process_multi_f64(rh._h, inp, C, n, outp, cap, counts.ctypes.data)
+            if st != 0:
+                raise RuntimeError(f"gar_process_multi_f64: {st}")
+        rh.FlushMulti()
+
+    host_pass()
+    t0 = time.perf_counter()
+    host_pass()
+    dt_host = time.perf_counter() - t0
+    return {
+        "chunk_frames": chunk,
+        "device_api": {"value": round(frames * C / dt_dev / 1e6, 2), "unit": "Msamples/s", "calls": ncalls,
+                       "us_per_call": round(dt_dev / ncalls * 1e6, 2),
+                       "sample": f"{frames / w['ir']:.0f} s of the stream, gar_process_device per chunk + flush, "
+                                 "inputs in HBM, one synchronise at the end"},
+        "host_cabi": {"value": round(hframes * C / dt_host / 1e6, 2), "unit": "Msamples/s", "calls": len(calls),
+                      "us_per_call": round(dt_host / max(len(calls), 1) * 1e6, 2),
+                      "sample": f"{hs:.0f} s, gar_process_multi_f64 per chunk from planar float64 host buffers "
+                                "(H2D + launches + D2H + synchronise per call, PCIe-inclusive)"},
+    }
 
 
 if __name__ == "__main__":
