@@ -180,7 +180,7 @@ bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
     s.f64 = f64;
     hx = hx && !f64;
     const EngineDesign& d = s.d;
-    if (d.kind == EngineKind::Cubic) { err = "QualityQuick cubic stage is not supported on the GPU path yet"; return false; }
+    if (d.kind == EngineKind::Cubic) return true;  // no filter banks (cubic.go:75-90)
     if (d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) {
         if (!buildBgPlan(firFromDft(d.dft), f64, s.dftP)) { err = "DFT plan"; return false; }
         s.dftD = uploadPlan(s.dftP, s.dftA, s.dftT, dry);
@@ -218,6 +218,7 @@ bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
 
 // StageAdapter.GetLatency (internal/engine/stage_adapter.go:43-57)
 int stageLatency(const EngineDesign& d) {
+    if (d.kind == EngineKind::Cubic) return 2;  // cubicLatencySamples (internal/engine/constants.go:12)
     int lat = 0;
     if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1)
         lat += (d.dft.taps * d.dft.factor) / 2;
@@ -239,6 +240,7 @@ struct Counters {
     int64_t dec_hist = 0;      // len(DFTDecimationStage.history)
     int dec_phase = 0;         // DFTDecimationStage.decimPhase
     int64_t y_count = 0;       // samples emitted
+    double cub_phase = 0.0;    // CubicStage.phase (cubic.go:17)
 };
 
 // DFTStage.processZeroCopy counts (dft_stage.go:156-207)
@@ -291,6 +293,25 @@ int64_t cntDecim(Counters& s, const DecimBank& b, int64_t n) {
     return nout;
 }
 
+// CubicStage.Process walk (cubic.go:42-61): the f64 phase recurrence, run once for
+// all channels; `segs` (when given) receives the state every kCubicSegInputs inputs.
+int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* segs) {
+    const double step = 1.0 / ratio;
+    double ph = s.cub_phase;
+    int64_t nout = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (segs && i % kCubicSegInputs == 0) segs->push_back({ph, s.y_count + nout, s.x_count + i});
+        while (ph < 1.0) {
+            ++nout;
+            ph += step;
+        }
+        ph -= 1.0;
+    }
+    s.cub_phase = ph;
+    s.x_count += n;
+    return nout;
+}
+
 // ---------------------------------------------------------------------------
 struct Hist {
     DevBuf buf[2];
@@ -320,12 +341,61 @@ struct OutView {
     int f64 = 0;
 };
 
+// Pinned host buffer the device reads in place (CubicStage checkpoints); reused only
+// after the launch that read it has completed (event).
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    PinBuf() = default;
+    PinBuf(const PinBuf&) = delete;
+    PinBuf& operator=(const PinBuf&) = delete;
+    PinBuf(PinBuf&& o) noexcept : p(o.p), cap(o.cap), ev(o.ev), pending(o.pending) { o.p = nullptr; o.ev = nullptr; o.cap = 0; o.pending = false; }
+    PinBuf& operator=(PinBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p; cap = o.cap; ev = o.ev; pending = o.pending;
+            o.p = nullptr; o.ev = nullptr; o.cap = 0; o.pending = false;
+        }
+        return *this;
+    }
+    ~PinBuf() { release(); }
+    void release() {
+        if (ev) { (void)hipEventSynchronize(ev); (void)hipEventDestroy(ev); }
+        if (p) (void)hipHostFree(p);
+        p = nullptr; ev = nullptr; cap = 0; pending = false;
+    }
+    // Wait for the previous reader, grow if needed; returns the host pointer.
+    void* acquire(size_t bytes) {
+        if (pending) HIPCHK(hipEventSynchronize(ev));
+        pending = false;
+        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (bytes > cap) {
+            if (p) HIPCHK(hipHostFree(p));
+            p = nullptr;
+            cap = 0;
+            const size_t nb = bytes + bytes / 2 + 4096;
+            HIPCHK(hipHostMalloc(&p, nb, hipHostMallocDefault));
+            cap = nb;
+        }
+        return p;
+    }
+    void issued(hipStream_t s) {
+        HIPCHK(hipEventRecord(ev, s));
+        pending = true;
+    }
+};
+
 struct Group {
     int c0 = 0, C = 1;
     std::vector<Counters> cnt;
     std::vector<StageDev> dev;
     std::vector<DevBuf> tmp;   // per stage-boundary output buffers
     DevBuf utmp;               // staged DFT output (u) scratch
+    PinBuf cubPin[2];          // CubicStage checkpoints, double-buffered
+    int cubCur = 0;
+    std::vector<CubicSeg> cubSegs;
 };
 
 }  // namespace
@@ -470,6 +540,27 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
     const int64_t n = in.n;
     if (n == 0) return 0;
     switch (d.kind) {
+        case EngineKind::Cubic: {
+            // CubicStage.Process (cubic.go:33-64); Flush emits nothing (cubic.go:93-96)
+            const int64_t x0 = c.x_count;
+            std::vector<CubicSeg>* segs = x.launch ? &x.g->cubSegs : nullptr;
+            if (segs) segs->clear();
+            const SrcDesc src = mkSrc(dv.xh, C, x0, in);
+            const int64_t y0 = c.y_count;
+            const int64_t nout = cntCubic(c, d.ratio, n, segs);
+            if (x.launch && nout > 0) {
+                PinBuf& pb = x.g->cubPin[x.g->cubCur];
+                x.g->cubCur ^= 1;
+                void* hp = pb.acquire(segs->size() * sizeof(CubicSeg));
+                std::memcpy(hp, segs->data(), segs->size() * sizeof(CubicSeg));
+                HIPCHK(launchCubic(rt.f64 ? 1 : 0, static_cast<const CubicSeg*>(hp), static_cast<int64_t>(segs->size()),
+                                   c.x_count, 1.0 / d.ratio, src, mkOut(out, y0, nout), C, x.s));
+                pb.issued(x.s);
+            }
+            hist_update(x, dv.xh, src, std::max<int64_t>(0, c.x_count - 3), c.x_count);
+            c.y_count += nout;
+            return nout;
+        }
         case EngineKind::Passthrough: {
             if (x.launch && !in.zeros)
                 HIPCHK(launchCopy(in.p, in.f64, in.fs, in.cs, out.p, out.f64, out.fs, out.cs, n, C, x.s));
@@ -903,7 +994,7 @@ gar_status addStage(Handle* h, double inRate, double outRate, Quality q) {
     if (!designEngine(inRate, outRate, q, rt->d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
     if (!buildStage(*rt, h->f64, h->hx, h->dry, err)) {
         g_err = err;
-        return rt->d.kind == EngineKind::Cubic ? GAR_ERR_NOT_SUPPORTED : GAR_ERR_INTERNAL;
+        return GAR_ERR_INTERNAL;
     }
     h->stages.push_back(std::move(rt));
     return GAR_OK;
@@ -934,8 +1025,10 @@ gar_status newCommon(gar_config* cfg, int32_t nstreams, gar_resampler** out) {
         for (const StageSpec& sp : specs) {
             // createStage -> engine.NewResampler[float64](48000, 48000*ratio, q) (stages.go:54-70)
             if (sp.type == StageType::Cubic) {
-                g_err = "QualityQuick (cubic) pipelines are not supported on the GPU path yet";
-                return GAR_ERR_NOT_SUPPORTED;
+                // newCubicStage(ratio) -> engine.NewCubicStage[float64] at the total ratio (stages.go:21-23)
+                st = addStage(h.get(), 1.0, sp.ratio, Quality::Quick);
+                if (st != GAR_OK) return st;
+                continue;
             }
             const double ir = 48000.0;
             st = addStage(h.get(), ir, ir * sp.ratio, precisionToEngineQuality(prec));
@@ -1346,10 +1439,17 @@ gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
         int len = 0;
         if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1) len += d.dft.taps * d.dft.factor;
         if (d.kind == EngineKind::DftPoly) len += d.poly.taps * d.poly.L;
-        info->filter_length = len;
-        info->phases = d.kind == EngineKind::DftPoly ? d.poly.L : 0;
-        info->simd_enabled = 1;
-        std::snprintf(info->simd_type, sizeof(info->simd_type), "%s", "gfx950 MFMA (HIP)");
+        if (d.kind == EngineKind::Cubic) {
+            // CubicStage: 4 points, no phases, no SIMD info (cubic.go:119-137)
+            info->filter_length = 4;
+            info->phases = 0;
+            info->memory_usage += 64 * r->channels;
+        } else {
+            info->filter_length = len;
+            info->phases = d.kind == EngineKind::DftPoly ? d.poly.L : 0;
+            info->simd_enabled = 1;
+            std::snprintf(info->simd_type, sizeof(info->simd_type), "%s", "gfx950 MFMA (HIP)");
+        }
     }
     return GAR_OK;
 }

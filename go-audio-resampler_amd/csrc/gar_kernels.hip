@@ -5,6 +5,7 @@
 //                reference engine: DFT xf upsampler (dft_stage.go:229-273),
 //                integer decimator (dft_stage.go:525-534), and the fused
 //                DFT x2 -> polyphase composite (gar_plan.cpp firComposite).
+//  cubic_kernel  QualityQuick CubicStage (cubic.go:33-90) over host-checkpointed phase walks.
 //  poly_kernel   polyphase stage with live cubic coefficient interpolation
 //                (polyphase_stage.go:257-293) for ratios whose fixed-point
 //                step has fractional bits (x != 0).
@@ -145,6 +146,59 @@ hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& od, i
     if (blocks > 65536) blocks = 65536;
     if (p.f64) hipLaunchKernelGGL(poly_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p, src, od, nout, C);
     else hipLaunchKernelGGL(poly_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p, src, od, nout, C);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// CubicStage (QualityQuick, internal/engine/cubic.go:33-90): 4-point cubic
+// interpolation at a floating-point phase.  The phase walk is a sequential f64
+// recurrence (phase += 1/ratio per output, -= 1 per input); the host runs it
+// once for all channels and checkpoints its exact state every kCubicSegInputs
+// inputs; one thread per (segment, channel) re-walks its segment with the same
+// f64 operations, so every output sits at the reference's phase bit for bit.
+// ---------------------------------------------------------------------------
+template <class TC>
+__global__ __launch_bounds__(256) void cubic_kernel(const CubicSeg* segs, int64_t nseg, int64_t x_end, double step,
+                                                    SrcDesc src, OutDesc od, int C) {
+#pragma clang fp contract(off)
+    const int64_t total = nseg * C;
+    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; idx < total;
+         idx += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t sgi = idx / C;
+        const int c = static_cast<int>(idx - sgi * C);
+        const CubicSeg sg = segs[sgi];
+        const int64_t i1 = min(sg.i + kCubicSegInputs, x_end);
+        // history[3..1] = inputs i-3 .. i-1 (zeros before the stream start)
+        double h3 = static_cast<double>(srcRead<TC>(src, sg.i - 3, c));
+        double h2 = static_cast<double>(srcRead<TC>(src, sg.i - 2, c));
+        double h1 = static_cast<double>(srcRead<TC>(src, sg.i - 1, c));
+        double ph = sg.phase;
+        int64_t o = sg.o;
+        for (int64_t i = sg.i; i < i1; ++i) {
+            const double h0 = static_cast<double>(srcRead<TC>(src, i, c));
+            while (ph < 1.0) {
+                // s[-1], s[0], s[1], s[2] = history[3], [2], [1], [0] (cubic.go:78-89)
+                const double b = 0.5 * (h1 + h3) - h2;
+                const double a = (1.0 / 6.0) * (h0 - h1 + h3 - h2 - 4 * b);
+                const double cc = h1 - h2 - a - b;
+                outWrite<TC>(od, o, c, static_cast<TC>(((a * ph + b) * ph + cc) * ph + h2));
+                ++o;
+                ph += step;
+            }
+            ph -= 1.0;
+            h3 = h2; h2 = h1; h1 = h0;
+        }
+    }
+}
+
+hipError_t launchCubic(int f64, const CubicSeg* segs, int64_t nseg, int64_t x_end, double step, const SrcDesc& src,
+                       const OutDesc& od, int C, hipStream_t stream) {
+    if (nseg <= 0) return hipSuccess;
+    const int64_t total = nseg * C;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (f64) hipLaunchKernelGGL(cubic_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, segs, nseg, x_end, step, src, od, C);
+    else hipLaunchKernelGGL(cubic_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, segs, nseg, x_end, step, src, od, C);
     return hipGetLastError();
 }
 

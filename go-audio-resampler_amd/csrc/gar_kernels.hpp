@@ -73,6 +73,15 @@ struct PolyDev {
     const void *a, *b, *c, *d;  // [L][T] reversed, compute dtype
 };
 
+// CubicStage checkpoint (cubic.go:42-61): before input i (absolute stage-input
+// index) the phase is `phase` and the next output index is o.  Checkpoints are
+// kCubicSegInputs inputs apart.
+struct CubicSeg {
+    double phase;
+    int64_t o, i;
+};
+constexpr int64_t kCubicSegInputs = 256;
+
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
@@ -80,6 +89,10 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int 
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
                       hipStream_t stream);
+// CubicStage outputs of nseg checkpointed segments (segs readable by the device:
+// pinned host or device memory); x_end = one past the last input; step = 1/ratio.
+hipError_t launchCubic(int f64, const CubicSeg* segs, int64_t nseg, int64_t x_end, double step, const SrcDesc& src,
+                       const OutDesc& od, int C, hipStream_t stream);
 // dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.
 hipError_t launchGather(int f64, const SrcDesc& src, void* dst, int64_t t0, int64_t n, int C, hipStream_t stream);
 // Strided copy with dtype conversion (pass-through stages, group split).

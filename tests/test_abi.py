@@ -73,9 +73,13 @@ def test_new_expands_preset_into_config(gar):  # resample.go:282-284 mutates the
     gar.lib().gar_free(h)
 
 
-def test_quick_preset_not_supported_yet(gar):
-    with pytest.raises(gar.ErrNotSupported):
-        gar.New(gar.Config(44100, 48000, 1, gar.QualityQuick, DryRun=True))
+def test_quick_preset_builds_cubic_stage(gar, O):
+    """QualityQuick: one CubicStage at the total ratio (pipeline.go:115-121, stages.go:21-23)."""
+    g = gar.New(gar.Config(44100, 48000, 1, gar.QualityQuick, DryRun=True))
+    ref = O.NewResampler(44100, 48000, 1, 0)
+    assert g.GetLatency() == ref.latency()
+    info = g.GetInfo()
+    assert (info.FilterLength, info.Phases, bool(info.SIMDEnabled)) == (4, 0, False)  # cubic.go:119-137
 
 
 ENGINE_PAIRS = [(44100, 48000), (48000, 44100), (48000, 96000), (96000, 48000), (48000, 16000), (16000, 44100),
@@ -83,7 +87,7 @@ ENGINE_PAIRS = [(44100, 48000), (48000, 44100), (48000, 96000), (96000, 48000), 
 
 
 @pytest.mark.parametrize("i,o", ENGINE_PAIRS)
-@pytest.mark.parametrize("preset", [1, 2, 3])
+@pytest.mark.parametrize("preset", [0, 1, 2, 3])
 def test_engine_stream_lengths(gar, O, i, o, preset):
     """Every call returns exactly the reference's sample count: chunked Process,
     Flush, Process after Flush without Reset, repeated Flush, Reset."""
@@ -110,7 +114,7 @@ NEW_PAIRS = [(44100, 48000), (48000, 44100), (96000, 44100), (96000, 16000), (19
 
 
 @pytest.mark.parametrize("i,o", NEW_PAIRS)
-@pytest.mark.parametrize("preset", [1, 2, 3, 4])
+@pytest.mark.parametrize("preset", [0, 1, 2, 3, 4])
 def test_new_path_stream_lengths(gar, O, i, o, preset):
     rng = np.random.default_rng(1)
     ref = O.NewResampler(i, o, 1, preset)

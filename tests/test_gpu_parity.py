@@ -98,7 +98,7 @@ ENGINE_CASES = [
 
 
 @pytest.mark.parametrize("i,o", ENGINE_CASES)
-@pytest.mark.parametrize("preset", [gar_q for gar_q in (1, 3)])
+@pytest.mark.parametrize("preset", [0, 1, 3])
 def test_engine_f64_vs_oracle(gar, O, cuda, i, o, preset):
     x = signal(int(i * 0.3) + 17, 1, i, seed=i % 97)[:, 0]
     r = gar.NewEngine(i, o, preset)
@@ -285,3 +285,41 @@ def test_device_api_float64_io_on_f32_compute(gar, O, cuda):
     want = oracle_new(O, 44100, 48000, x, O.P_HIGH)
     for c in range(2):
         check(got[:, c], want[c], F32_RMS_TOL)
+
+
+QUICK_CASES = [(44100, 48000), (48000, 44100), (16000, 44100), (96000, 8000), (8000, 96000), (44100, 44100),
+               (22050, 16000)]
+
+
+@pytest.mark.parametrize("i,o", QUICK_CASES)
+def test_quick_cubic_new_path_streaming(gar, O, cuda, i, o):
+    """QualityQuick (CubicStage, cubic.go:33-90; pipeline.go:115-121) through the device API in
+    ragged chunks: exact output counts, float64 within 1e-12 of the oracle, float32 compute
+    within 1e-6 of the oracle fed the same float32 samples."""
+    x = signal(i // 3 + 5, 2, i, seed=7)
+    chunks = [1, 2, 3, 4096, 1000, 0, 17]
+    chunks += chunk_sizes(len(x) - sum(chunks), 4096)
+    for dt, tdt, tol in ((gar.F64, cuda.float64, F64_RMS_TOL), (gar.F32, cuda.float32, F32_RMS_TOL)):
+        xin = x if dt == gar.F64 else x.astype(np.float32).astype(np.float64)
+        want = oracle_new(O, i, o, xin, 0, chunks=chunks)
+        r = gar.New(gar.Config(i, o, 2, gar.QualityQuick, ComputeDtype=dt))
+        xd = cuda.from_numpy(xin).to(device="cuda", dtype=tdt)
+        outs, s = [], 0
+        for n in chunks:
+            outs.append(r.process_device(xd[s:s + n]) if n else xd[:0])
+            s += n
+        outs.append(r.flush_device(dtype=tdt))
+        y = cuda.cat(outs).double().cpu().numpy()
+        for c in range(2):
+            assert y.shape[0] == len(want[c])
+            assert rms(y[:, c], want[c]) <= tol
+
+
+def test_quick_engine_float32(gar, O, cuda):
+    """NewEngineFloat32 with QualityQuick: CubicStage[float32] (cubic.go:15-90)."""
+    x = signal(30011, 1, 44100, seed=9)[:, 0].astype(np.float32)
+    got = gar.ResampleMonoFloat32(x, 44100, 48000, gar.QualityQuick)
+    e = O.Engine(44100, 48000, O.lib().o_preset_to_engine_quality(0), f32=True)
+    want = np.concatenate([e.process(x), e.flush()])
+    assert len(got) == len(want)
+    assert rms(got, want) <= F32_RMS_TOL

@@ -101,7 +101,7 @@ def test_go_fft_matches_numpy():
 
 
 # ----------------------------------------------------------------------------- GPU: HIP path
-GPU_CASES = [c for c in Q.THD_CASES if c[2] != "Quick"]
+GPU_CASES = list(Q.THD_CASES)  # QualityQuick included: CubicStage kernel (cubic.go:33-90)
 
 
 def _gpu_run(gar, ir, orr, q, dtype):
@@ -123,7 +123,7 @@ def test_gpu_f64_quality_equals_oracle(gar, O, cuda, ir, orr, name):
     thd = Q.thd_internal(g, ir, orr)
     assert abs(thd - Q.thd_internal(o, ir, orr)) <= GPU_F64_DB
     assert thd <= Q.MAX_THD[name]
-    if (ir, orr) == (44100, 48000):
+    if (ir, orr) == (44100, 48000) and name in Q.README_THD_44K1_48K:
         assert abs(thd - Q.README_THD_44K1_48K[name]) <= PIN_DB
     assert abs(Q.snr_internal(g, ir, orr) - Q.snr_internal(o, ir, orr)) <= GPU_SNR_DB
 
@@ -142,8 +142,7 @@ def test_gpu_f32_quality(gar, O, cuda, ir, orr, name, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["F64", "F32", "F32_EXACT"])
-@pytest.mark.parametrize("ir,orr,name", [c for c in Q.RIPPLE_CASES if c[2] != "Quick"],
-                         ids=_ids([c for c in Q.RIPPLE_CASES if c[2] != "Quick"]))
+@pytest.mark.parametrize("ir,orr,name", Q.RIPPLE_CASES, ids=_ids(Q.RIPPLE_CASES))
 def test_gpu_ripple_and_dc(gar, O, cuda, ir, orr, name, dtype):
     q = Q.ENGINE_Q[name]
     g = _gpu_run(gar, ir, orr, q, getattr(gar, dtype))
