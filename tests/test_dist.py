@@ -52,3 +52,50 @@ def test_shards_partition_streams(world):
         lo, hi = bench.shard_streams(1024, r, world)
         seen.extend(range(lo, hi))
     assert seen == list(range(1024))
+
+
+def _worker_resample(rank, world, port, q):
+    """Each rank resamples its contiguous shard of config 4's streams (dry-run handle: the host
+    state machine, exact reference counts, no GPU) in 4096-frame ProcessMulti calls + FlushMulti,
+    then the counters go through bench.reduce_stats (the only collective)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import gar
+    from helpers import chunk_sizes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    streams, frames = 64, 44_100  # config 4's shape at 1/16 of the streams and 1/10 of the length
+    lo, hi = bench.shard_streams(streams, rank, world)
+    r = gar.NewBatch(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True), hi - lo)
+    out = 0
+    for n in chunk_sizes(frames, 4096):
+        xs = [np.zeros(n)] * (2 * (hi - lo))
+        out += sum(len(y) for y in r.ProcessMulti(xs))
+    out += sum(len(y) for y in r.FlushMulti())
+    _, total = bench.reduce_stats(1.0, out, device=torch.device("cpu"))
+    q.put((rank, hi - lo, out, total))
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_resample_shards(O):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_resample, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the reference's own count for one stream, every stream identical
+    ref = O.NewResampler(44100, 48000, 1, O.P_HIGH)
+    per_channel = sum(len(ref.process(__import__("numpy").zeros(n), 0)) for n in [4096] * 10 + [44_100 - 40_960])
+    per_channel += len(ref.flush(0))
+    (_, n0, out0, t0), (_, n1, out1, t1) = res
+    assert (n0, n1) == (32, 32)
+    assert out0 == out1 == 32 * 2 * per_channel
+    assert t0 == t1 == 64 * 2 * per_channel
