@@ -1428,12 +1428,22 @@ gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
     std::memset(info, 0, sizeof(*info));
     std::snprintf(info->algorithm, sizeof(info->algorithm), "%s", "multi-stage");
     info->latency = gar_get_latency(r);
-    int64_t mem = 0;
-    for (const auto& s : r->stages)
-        mem += static_cast<int64_t>(s->fusedA.cap + s->dftA.cap + s->decimA.cap + s->pa.cap * 4);
-    for (const auto& g : r->groups)
-        for (const auto& d : g.dev) mem += static_cast<int64_t>(d.xh.buf[0].cap + d.xh.buf[1].cap + d.uh.buf[0].cap + d.uh.buf[1].cap);
-    info->memory_usage = mem;
+    // MemoryUsage as the reference counts it per channel (constant.go:457-466): the ring
+    // buffers between stages (default capacity 8192 float64, pipeline constants.go:55) plus each
+    // stage's coefficient tables and delay line (StageAdapter.GetMemoryUsage,
+    // stage_adapter.go:66-96); here the tables are shared by all channels on the device, but
+    // the figure keeps the reference's per-channel accounting.
+    const int64_t es = r->f64 ? 8 : 4;
+    int64_t perCh = static_cast<int64_t>(r->stages.size() + 1) * 8192 * 8;
+    for (const auto& s : r->stages) {
+        const EngineDesign& d = s->d;
+        if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1)
+            perCh += static_cast<int64_t>(d.dft.factor) * d.dft.taps * es + static_cast<int64_t>(d.dft.taps) * es;
+        if (d.kind == EngineKind::DftPoly)
+            perCh += 4 * static_cast<int64_t>(d.poly.L) * d.poly.taps * es + static_cast<int64_t>(d.poly.taps) * es;
+        if (d.kind == EngineKind::Decim) perCh += 2 * static_cast<int64_t>(d.decim.taps) * es;
+    }
+    info->memory_usage = perCh * r->channels;
     if (!r->stages.empty()) {
         const EngineDesign& d = r->stages[0]->d;
         int len = 0;
@@ -1443,7 +1453,7 @@ gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
             // CubicStage: 4 points, no phases, no SIMD info (cubic.go:119-137)
             info->filter_length = 4;
             info->phases = 0;
-            info->memory_usage += 64 * r->channels;
+            info->memory_usage += 64 * r->channels;  // cubicMemoryUsage (internal/engine/constants.go:15)
         } else {
             info->filter_length = len;
             info->phases = d.kind == EngineKind::DftPoly ? d.poly.L : 0;

@@ -206,3 +206,24 @@ def test_engine_quality_constructor_dry(gar):
     h = C.c_void_p(0)
     assert gar.lib().gar_new_engine_quality(44100.0, 48000.0, 42, gar.F64, C.byref(h)) == gar.INVALID_CONFIG
     assert not h.value
+
+
+@pytest.mark.parametrize("i,o", [(44100, 48000), (48000, 44100), (96000, 44100), (16000, 44100), (48000, 96000)])
+@pytest.mark.parametrize("preset", [0, 1, 3, 4])
+def test_get_info_fields(gar, O, i, o, preset):
+    """GetInfo (constant.go:452-485): algorithm, latency, and the primary stage's filter
+    length / phases (StageAdapter.GetFilterLength/GetPhases, stage_adapter.go:98-119;
+    CubicStage 4 / 0, cubic.go:119-132) against the oracle's stage designs."""
+    g = gar.New(gar.Config(i, o, 2, preset, DryRun=True))
+    ref = O.NewResampler(i, o, 1, preset)
+    inf = g.GetInfo()
+    assert inf.Algorithm == b"multi-stage"
+    assert inf.Latency == ref.latency()
+    s0 = ref.stage_info(0)
+    if s0.kind == 0:
+        assert (inf.FilterLength, inf.Phases) == (4, 0)
+    else:
+        want = (s0.dft_taps_per_phase * s0.dft_factor if s0.dft_factor > 1 else 0) + \
+            s0.poly_taps_per_phase * s0.poly_phases
+        assert (inf.FilterLength, inf.Phases) == (want, s0.poly_phases)
+    assert inf.MemoryUsage > 0

@@ -323,3 +323,27 @@ def test_quick_engine_float32(gar, O, cuda):
     want = np.concatenate([e.process(x), e.flush()])
     assert len(got) == len(want)
     assert rms(got, want) <= F32_RMS_TOL
+
+
+@pytest.mark.parametrize("dtype", ["F64", "F32"])
+@pytest.mark.parametrize("i,o,preset", [(44100, 48000, 3), (48000, 44100, 4), (96000, 44100, 4), (44100, 48000, 0)])
+def test_new_path_process_float32_values(gar, O, cuda, i, o, preset, dtype):
+    """New-path ProcessFloat32 / ProcessFloat32Into (constant.go:121-199): float32 in and out,
+    the float64 pipeline in between; values within 1e-6 of the oracle fed the same float32
+    samples, chunked Into calls identical to one-shot ProcessFloat32."""
+    x = signal(i // 4 + 3, 1, i, seed=11)[:, 0].astype(np.float32)
+    ref = O.NewResampler(i, o, 1, preset)
+    want = np.concatenate([ref.process(x.astype(np.float64), 0), ref.flush(0)])
+    r = gar.New(gar.Config(i, o, 1, preset, ComputeDtype=getattr(gar, dtype)))
+    got = np.concatenate([r.ProcessFloat32(x), r.Flush()])
+    assert got.dtype in (np.float32, np.float64)
+    check(got.astype(np.float64), want, F32_RMS_TOL)
+    r.Reset()
+    outs = []
+    for s, n in zip(range(0, len(x), 4096), chunk_sizes(len(x), 4096)):
+        buf = np.empty(r.EstimateOutput(n), dtype=np.float32)
+        k = r.ProcessFloat32Into(x[s:s + n], buf)
+        outs.append(buf[:k].copy())
+    outs.append(np.asarray(r.Flush(), dtype=np.float32))
+    into = np.concatenate(outs)
+    assert np.array_equal(into.astype(np.float32), got.astype(np.float32))
