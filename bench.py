@@ -46,10 +46,11 @@ PEAK_HBM_GBPS = 8000.0
 PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
 PEAK_F64_MATRIX_TFLOPS = 78.6
 # reference-algorithm flops per input sample
-REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6}
+REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6, "poly": None,
+                  "quick": None}
 DECIM_MACS_PER_INPUT = 611.5  # cfg5 stage 1: factor 2, 1223 taps
 # New path: preset -> precision -> engine quality (stages.go:54-70, pipeline_builder.go:76-100)
-ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit}
+ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit, "Quick": lambda g: g.EngineQuick}
 
 WORKLOADS = {
     "cfg2": dict(name="cfg2_stereo_f32_44k1_48k_q24_600s", ir=44100, orr=48000, ch=2, preset="High", seconds=600.0,
@@ -70,6 +71,14 @@ WORKLOADS = {
                  seconds=60.0, io="f64", compute="F64", streams=1, scaling="weak", chunk=4800,
                  desc="BASELINE configs[4]: 8-channel float64 96k->44.1k QualityVeryHigh multi-stage pipeline "
                       "(decimator x1/2 -> DFT x2 -> polyphase), 60 s streamed in 4800-frame ProcessInto chunks"),
+    # x != 0 polyphase (live cubic coefficients, poly_kernel) and QualityQuick (cubic_kernel)
+    "poly": dict(name="poly_stereo_f32_16k_44k1_q24_600s", ir=16000, orr=44100, ch=2, preset="High", seconds=600.0,
+                 io="f32", compute="F32", streams=1, scaling="weak", chunk=0, kind_bytes={4: 4 * (4 + 2.75625)},
+                 desc="stereo float32 16k->44.1k QualityHigh: DFT x2 stage, then DFT x2 + polyphase with a "
+                      "fractional step (x != 0, poly_kernel), 600 s, one Process+Flush"),
+    "quick": dict(name="quick_stereo_f32_44k1_48k_600s", ir=44100, orr=48000, ch=2, preset="Quick", seconds=600.0,
+                  io="f32", compute="F32", streams=1, scaling="weak", chunk=0, kind_bytes={5: 4 * (1 + 48000 / 44100)},
+                  desc="stereo float32 44.1k->48k QualityQuick (CubicStage), 600 s, one Process+Flush"),
 }
 
 
@@ -333,7 +342,7 @@ def main():
         step()
     torch.cuda.synchronize()
     r.profile(True)
-    for k in range(4):
+    for k in range(6):
         r.profile_read(k)
     if world > 1:
         torch.distributed.barrier()
@@ -345,7 +354,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    prof = {k: r.profile_read(k) for k in range(4)}
+    prof = {k: r.profile_read(k) for k in range(6)}
     r.profile(False)
 
     local_samples = frames * C * args.steps
@@ -392,13 +401,24 @@ def main():
             rms_tail = float(np.sqrt(np.mean(errs)))
 
     # roofline of the dominant kernel (HIP events on the launch stream, inside the library)
-    kinds = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)"}
-    dom = max((0, 1, 2), key=lambda k: prof[k][0])
+    kinds = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)",
+             4: "polyphase with live cubic coefficients (poly_kernel)", 5: "QualityQuick cubic stage (cubic_kernel)"}
+    dom = max((0, 1, 2, 4, 5), key=lambda k: prof[k][0])
     kms, launches = prof[dom]
     launch_s = (kms / 1e3) / max(launches, 1)
     in_bytes = 4 if w["io"] == "f32" else 8
     out_samples_step = (n_proc + n_tail) * C
-    if w["compute"] == "F32":
+    if w["compute"] == "F32" and dom in w.get("kind_bytes", {}):
+        # that stage's own stream bytes per input frame and channel (its input read once, output written once)
+        algo_bytes = w["kind_bytes"][dom] * frames * C
+        algo_per_launch = algo_bytes / max(launches / args.steps, 1)
+        achieved = algo_per_launch / launch_s / 1e9 if launches else None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
+        kernel_keys = ["poly_kernel"] if dom == 4 else ["cubic_kernel"]
+        kname = kinds[dom]
+        algo_unit_bytes = algo_per_launch
+    elif w["compute"] == "F32":
         # HBM-bound streaming FIR: algorithmic bytes = input read once + output written once
         algo_bytes = frames * C * in_bytes + n_proc * C * in_bytes
         algo_per_launch = algo_bytes / max(launches / args.steps, 1)
@@ -425,6 +445,7 @@ def main():
         kname = f"bg_kernel<double> ({kinds[dom]}, v_mfma_f64_16x16x4_f64)"
         algo_unit_bytes = None
     roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[args.workload]
+    roof["kernel_ms_by_kind"] = {kinds[k]: round(prof[k][0] / args.steps, 4) for k in prof if prof[k][1]}
     roof.update({"traffic": None, "kernel": kname, "kernel_kind": kinds[dom],
                  "kernel_ms_per_launch": round(launch_s * 1e3, 5), "launches": launches})
     if algo_unit_bytes:

@@ -430,8 +430,8 @@ struct gar_resampler {
     struct Ev { int tag; hipEvent_t a, b; };
     std::vector<Ev> events;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evPool;
-    double profiledMs[4] = {0, 0, 0, 0};
-    int64_t profiledLaunches[4] = {0, 0, 0, 0};
+    double profiledMs[6] = {0, 0, 0, 0, 0, 0};
+    int64_t profiledLaunches[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace gar {
@@ -447,8 +447,10 @@ struct Ctx {
 };
 
 // launchBg bracketed by HIP events on the launch stream when profiling is on.
-hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
-    if (!x.h->profile) return launchBg(p, src, od, C, x.s);
+// A launch bracketed by HIP events on its stream when profiling is on (tag = gar_profile_read kind).
+template <class L>
+hipError_t timed(Ctx& x, int tag, L&& launch) {
+    if (!x.h->profile) return launch();
     hipEvent_t a, b;
     if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
         a = x.h->evPool.back().first;
@@ -459,10 +461,14 @@ hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const Ou
         HIPCHK(hipEventCreate(&b));
     }
     HIPCHK(hipEventRecord(a, x.s));
-    const hipError_t e = launchBg(p, src, od, C, x.s);
+    const hipError_t e = launch();
     HIPCHK(hipEventRecord(b, x.s));
     x.h->events.push_back({tag, a, b});
     return e;
+}
+
+hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
+    return timed(x, tag, [&] { return launchBg(p, src, od, C, x.s); });
 }
 
 SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
@@ -553,8 +559,10 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                 x.g->cubCur ^= 1;
                 void* hp = pb.acquire(segs->size() * sizeof(CubicSeg));
                 std::memcpy(hp, segs->data(), segs->size() * sizeof(CubicSeg));
-                HIPCHK(launchCubic(rt.f64 ? 1 : 0, static_cast<const CubicSeg*>(hp), static_cast<int64_t>(segs->size()),
-                                   c.x_count, 1.0 / d.ratio, src, mkOut(out, y0, nout), C, x.s));
+                HIPCHK(timed(x, 5, [&] {
+                    return launchCubic(rt.f64 ? 1 : 0, static_cast<const CubicSeg*>(hp), static_cast<int64_t>(segs->size()),
+                                       c.x_count, 1.0 / d.ratio, src, mkOut(out, y0, nout), C, x.s);
+                }));
                 pb.issued(x.s);
             }
             hist_update(x, dv.xh, src, std::max<int64_t>(0, c.x_count - 3), c.x_count);
@@ -621,7 +629,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                     PolyDev p = rt.polyD;
                     p.at0 = before.at;
                     p.u_base = before.u_base;
-                    HIPCHK(launchPoly(p, usrc, mkOut(out, y0, nout), nout, C, x.s));
+                    HIPCHK(timed(x, 4, [&] { return launchPoly(p, usrc, mkOut(out, y0, nout), nout, C, x.s); }));
                 }
                 hist_update(x, dv.xh, xsrc, c.x_count - c.dft_hist, c.x_count);
                 if (nu > 0) hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
@@ -707,7 +715,7 @@ int64_t stageFlush(Ctx& x, int si, const OutView& out) {
                     PolyDev p = rt.polyD;
                     p.at0 = before.at;
                     p.u_base = before.u_base;
-                    HIPCHK(launchPoly(p, usrc, mkOut(o2, y0, nout), nout, C, x.s));
+                    HIPCHK(timed(x, 4, [&] { return launchPoly(p, usrc, mkOut(o2, y0, nout), nout, C, x.s); }));
                 }
                 hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
                 c.y_count += nout;
@@ -1486,7 +1494,7 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
 }
 
 gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t* launches) {
-    if (!r || kind < 0 || kind > 3) return GAR_ERR_INVALID_ARGUMENT;
+    if (!r || kind < 0 || kind > 5) return GAR_ERR_INVALID_ARGUMENT;
     DeviceGuard dg(r->dry ? -1 : r->device);
     return wrap([&]() -> gar_status {
         for (auto& ev : r->events) {

@@ -99,9 +99,13 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
 
+    // small launches (stream chunks, flush tails): one macro period per column, each block's
+    // window gathered in one pass -- latency over bandwidth (knob GAR_HXS_SMALL=0/1 forces)
+    static const int knobSmall = std::getenv("GAR_HXS_SMALL") ? std::atoi(std::getenv("GAR_HXS_SMALL")) : -1;
+    const bool small = knobSmall >= 0 ? knobSmall == 1 : nmac * C <= static_cast<int64_t>(16) * 2 * ncu;
     // chunk length: about one block (16 columns) per CU
     const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
-    const int64_t nchunkT = std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
+    const int64_t nchunkT = small ? nmac : std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
     int64_t Np = std::max<int64_t>(1, cdiv(nmac, nchunkT));
     // raw loads address a chunk's rows with 32-bit offsets from the chunk's first row:
     // (Np*Qc + rows of one group + a piece) rows must span less than 2^31 bytes
@@ -111,7 +115,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     if (rawSpan) Np = std::min(Np, npMax);
     int64_t nchunk = cdiv(nmac, Np);
     // whole blocks where the channel count divides 16 (empty trailing chunks read zeros, store nothing)
-    if (16 % C == 0) nchunk = cdiv(nchunk * C, 16) * 16 / C;
+    if (16 % C == 0 && !small) nchunk = cdiv(nchunk * C, 16) * 16 / C;
     const int64_t ncols = nchunk * C;
     if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorNotSupported;
 
@@ -140,7 +144,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         return hxsLds(Rt, stageFor(G)) <= 160 * 1024 && 2 * dmas <= 32 && 4 * ((GQ + 63) / 64 * 64) <= kHxsConvMax * nth;
     };
     int G = 0, R = 0, Rt = 0, Wg = 0;
-    for (int cand = 3; cand >= 1; --cand) {
+    for (int cand = small ? 1 : 3; cand >= 1; --cand) {
         int r, rt, wg;
         ringFor(cand, r, rt, wg);
         if (cand > 1 && cand > Np) continue;
@@ -150,7 +154,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         break;
     }
     if (G == 0) return hipErrorNotSupported;
-    const int stageBytes = stageFor(G);
+    const int stageBytes = small ? 0 : stageFor(G);
 
     HxsArgs x{};
     x.A = static_cast<const h8v*>(p.A);
@@ -178,6 +182,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.fastHi = rawOk ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
     x.fmt = fmt;
     x.stageBytes = stageBytes;
+    x.small = small ? 1 : 0;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
     const int esz = od.f64 ? 8 : 4;
     x.out_f64 = od.f64;
@@ -203,8 +208,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.T1 = p.T1;
     x.T2 = p.T2;
     if (trace)
-        fprintf(stderr, "hxs: o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
-                (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
+        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
+                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
                 (long long)x.fastLo, (long long)x.fastHi);
     const size_t lds = hxsLds(Rt, stageBytes);
     const int64_t blocks = x.nblocks;

@@ -44,6 +44,7 @@ struct HxsArgs {
     int dbg;               // development attribution (GAR_HXS_DBG, wrong output): 1 no steady DMAs, 2 no stores,
                            // 4 no MFMA, 16 no steady conversion
     int stageBytes;        // raw LDS bytes of one stage (three buffers)
+    int small;             // one period per column, window staged in one pass (hxsSmallStage)
     int vst, fmt;          // epilogue layout (template VST), raw stage layout 0 gathered ROW16 / 1 STEREO / 2 ROW16 DMA
     int64_t a_lo, a_hi;    // absolute macro periods of the launch
     int64_t o_lo, o_hi;    // outputs written
@@ -379,6 +380,30 @@ __device__ __forceinline__ void hxsConvert(const HxsArgs& x, const HxsStage& st,
     }
 }
 
+// Small launches (x.small: one macro period per column, one group): every wave gathers
+// its share of the block's whole window [0, Wg) straight into the ring in one pass --
+// one memory round trip instead of the pipeline's chain of DMA stages.
+__device__ __forceinline__ void hxsSmallStage(const HxsArgs& x, int b, int tid, int nth, char* ring, uint32_t QS,
+                                              int* loudLo, int* loudHi, int* flag) {
+    const HxsArgsP xc = hxsCold();
+    const SrcDesc src = kload(&xc->src);
+    HxsStage st;
+    st.T0 = 0;
+    st.nrow = x.Wg;
+    st.fast = false;
+    for (int i = tid; i < 4 * x.Wg; i += nth) {
+        const int q = i & 3, row = i >> 2;
+        f32x4 e;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int col = b * 16 + 4 * q + n;
+            const int k = col / x.C, c = col - k * x.C;
+            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, row), c, x.A) : 0.f;
+        }
+        hxsPutItem(x, st, 0, q, row, e, ring, QS, loudLo, loudHi, flag);
+    }
+}
+
 template <int VST>
 __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y, int lane) {
     if (VST == 2) {
@@ -439,11 +464,12 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     const int nslot = x.R / GQ;
     unsigned long long tm = 0, tw = 0, tcv = 0;
 
-    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
+    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
 
     for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
         hxsBarrier();  // loud state reset; the previous block's ring reads done
-        hxsBarrier();  // load 0 landed
+        if (x.small) hxsSmallStage(x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        hxsBarrier();  // load 0 landed (small: the whole window in the ring)
         const int col = b * 16 + l16;
         const bool colOk = col < x.ncols;
         const int kcol = col / x.C, ccol = col - kcol * x.C;
@@ -557,16 +583,20 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
 __device__ __forceinline__ void hxsLoaders(const HxsArgs& x, const HxsShared& sh_, int wl, int lane) {
     const int GQ = x.G * x.Qc;
     const int tid = (x.nprog + wl) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
-    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
+    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
     unsigned long long tc = 0, tl = 0, tb = 0, ti = 0, tpre = 0, tloop = 0;
     const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
     for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
         if (wl == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
         if (wl == 0 && lane == 0) *sh_.flag = 0;
         hxsBarrier();  // loud state reset; the previous block's ring reads done
-        hxsIssue(x, hxsLoad(x, b, 0, P), b, wl, lane, sh_.raw);
-        hxsWaitVm(nL > 1 ? hxsIssue(x, hxsLoad(x, b, 1, P), b, wl, lane, sh_.raw + x.stageBytes) : 0);
-        hxsBarrier();  // load 0 landed
+        if (x.small) {
+            hxsSmallStage(x, b, tid, nth, sh_.ring, sh_.QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        } else {
+            hxsIssue(x, hxsLoad(x, b, 0, P), b, wl, lane, sh_.raw);
+            hxsWaitVm(nL > 1 ? hxsIssue(x, hxsLoad(x, b, 1, P), b, wl, lane, sh_.raw + x.stageBytes) : 0);
+        }
+        hxsBarrier();  // load 0 landed (small: the whole window in the ring)
         if (x.prof) tpre += __builtin_amdgcn_s_memrealtime() - rStart;
         for (int j = 0; j < P + x.ngroups; ++j) {
             const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;

@@ -110,42 +110,66 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
 // ---------------------------------------------------------------------------
 // General polyphase stage (cubic sub-phase interpolation live).
 // ---------------------------------------------------------------------------
+// A workgroup owns a tile of consecutive outputs: it first evaluates the
+// interpolated coefficients a + x(b + x(c + x d)) of every (output, tap) of the
+// tile ONCE into LDS (the reference evaluates them per channel inside
+// CubicInterpDot, polyphase_stage.go:283-289), then each thread accumulates
+// one (output, channel) dot product over the shared row -- consecutive threads
+// are consecutive channels of one output, so the input reads coalesce for
+// many channels and the taps of neighbouring outputs hit the same lines.
+// Per-tap arithmetic and summation order are those of the reference's loop.
+constexpr int kPolyThreads = 256;
+constexpr int kPolyLdsBytes = 48 * 1024;
+
 template <class TC>
-__global__ __launch_bounds__(256) void poly_kernel(PolyDev p, SrcDesc src, OutDesc od, int64_t nout, int C) {
-    const int64_t total = nout * C;
+__global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc src, OutDesc od, int64_t nout, int C,
+                                                            int MT) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+    TC* coef = reinterpret_cast<TC*>(psm);  // [MT][T]
     const TC* A = static_cast<const TC*>(p.a);
     const TC* B = static_cast<const TC*>(p.b);
     const TC* Cc = static_cast<const TC*>(p.c);
     const TC* D = static_cast<const TC*>(p.d);
     const TC fscale = static_cast<TC>(1.0 / 65536.0);
-    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; idx < total;
-         idx += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t m = idx / C;
-        const int c = static_cast<int>(idx - m * C);
-        const int64_t at = p.at0 + m * p.step;
-        const int64_t full = at >> 16;
-        const int64_t div = full / p.L;
-        const int ph = static_cast<int>(full % p.L);
-        const TC x = static_cast<TC>(at & 0xFFFF) * fscale;
-        const int64_t base = p.u_base + div;
-        const size_t o = static_cast<size_t>(ph) * p.T;
-        TC acc = 0;
-        for (int k = 0; k < p.T; ++k) {
-            const TC coef = A[o + k] + x * (B[o + k] + x * (Cc[o + k] + x * D[o + k]));
-            acc += srcRead<TC>(src, base + k, c) * coef;
+    const int T = p.T;
+    const int64_t ntiles = (nout + MT - 1) / MT;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t m0 = tile * MT;
+        const int mt = static_cast<int>(min<int64_t>(MT, nout - m0));
+        __syncthreads();  // previous tile's rows consumed
+        for (int e = threadIdx.x; e < mt * T; e += blockDim.x) {
+            const int mm = e / T, k = e - mm * T;
+            const int64_t at = p.at0 + (m0 + mm) * p.step;
+            const int ph = static_cast<int>((at >> 16) % p.L);
+            const TC x = static_cast<TC>(at & 0xFFFF) * fscale;
+            const size_t o = static_cast<size_t>(ph) * T + k;
+            coef[mm * T + k] = A[o] + x * (B[o] + x * (Cc[o] + x * D[o]));
         }
-        outWrite<TC>(od, od.o_lo + m, c, acc);
+        __syncthreads();
+        for (int e = threadIdx.x; e < mt * C; e += blockDim.x) {
+            const int mm = e / C, c = e - mm * C;
+            const int64_t at = p.at0 + (m0 + mm) * p.step;
+            const int64_t base = p.u_base + (at >> 16) / p.L;
+            const TC* row = coef + mm * T;
+            TC acc = 0;
+            for (int k = 0; k < T; ++k) acc += srcRead<TC>(src, base + k, c) * row[k];
+            outWrite<TC>(od, od.o_lo + m0 + mm, c, acc);
+        }
     }
 }
 
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& od, int64_t nout, int C,
                       hipStream_t stream) {
     if (nout <= 0) return hipSuccess;
-    const int64_t total = nout * C;
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    if (p.f64) hipLaunchKernelGGL(poly_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p, src, od, nout, C);
-    else hipLaunchKernelGGL(poly_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, p, src, od, nout, C);
+    const int es = p.f64 ? 8 : 4;
+    // outputs per tile: enough (output, channel) pairs for the block, rows within the LDS budget
+    int MT = std::max(1, (2 * kPolyThreads + C - 1) / C);
+    MT = std::min<int>(MT, std::max(1, kPolyLdsBytes / (p.T * es)));
+    const int64_t ntiles = (nout + MT - 1) / MT;
+    const int64_t blocks = std::min<int64_t>(ntiles, 8192);
+    const size_t lds = static_cast<size_t>(MT) * p.T * es;
+    if (p.f64) hipLaunchKernelGGL(poly_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(kPolyThreads), lds, stream, p, src, od, nout, C, MT);
+    else hipLaunchKernelGGL(poly_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(kPolyThreads), lds, stream, p, src, od, nout, C, MT);
     return hipGetLastError();
 }
 

@@ -287,7 +287,8 @@ class Resampler:
         lib().gar_profile_enable(self._h, int(on))
 
     def profile_read(self, kind=0):
-        """(total ms, launches) of one MFMA FIR kind (0 fused, 1 DFT, 2 decimator) since the last read."""
+        """(total ms, launches) of one kernel kind (0 fused FIR, 1 DFT FIR, 2 decimator FIR, 3 fused FIR
+        of a flush, 4 polyphase with cubic coefficients, 5 cubic stage) since the last read."""
         ms, n = C.c_double(0), C.c_int64(0)
         _check(lib().gar_profile_read(self._h, kind, C.byref(ms), C.byref(n)))
         return ms.value, n.value

@@ -185,7 +185,8 @@ const char *gar_last_error(void);                       /* thread-local detail f
 void gar_profile_enable(gar_resampler *r, int32_t on);
 /* Sum of launch durations (ms) and launch count of one kernel kind (0 fused
  * DFT+polyphase FIR, 1 DFT FIR, 2 decimator FIR, 3 fused FIR launched by a
- * flush) since its last read. */
+ * flush, 4 polyphase stage with live cubic coefficients, 5 QualityQuick cubic
+ * stage) since its last read. */
 gar_status gar_profile_read(gar_resampler *r, int32_t kind, double *ms, int64_t *launches);
 
 /* ---- host-only design introspection (no GPU needed) ----------------------- */
