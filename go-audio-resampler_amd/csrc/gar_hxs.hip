@@ -107,6 +107,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
     const int64_t nchunkT = small ? nmac : std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
     int64_t Np = std::max<int64_t>(1, cdiv(nmac, nchunkT));
+    static const int knobNp = std::getenv("GAR_HXS_NP") ? std::atoi(std::getenv("GAR_HXS_NP")) : 0;
+    if (knobNp > 0 && !small) Np = knobNp;  // development: chunk length in macro periods
     // raw loads address a chunk's rows with 32-bit offsets from the chunk's first row:
     // (Np*Qc + rows of one group + a piece) rows must span less than 2^31 bytes
     const int64_t rowBytes = std::max<int64_t>(4, src.in_fs * 4);
@@ -138,8 +140,11 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const int RPc = fmt == 1 ? 128 : 16, pieceBytes = fmt == 1 ? 8192 : 1024, dmaPerPiece = fmt == 1 ? 8 : 1;
     auto stageFor = [&](int G) { return (G * static_cast<int>(Qc) + RPc - 1) / RPc * pieceBytes; };
     const int nth = 64 * (p.nw + kHxsLoaders);
+    // register staging (default; -DGAR_HXS_DMA builds the LDS-DMA raw-buffer pipeline)
+    const bool regs = kHxsRegs && !small;
     auto fits = [&](int G, int Rt) {
         const int GQ = G * static_cast<int>(Qc);
+        if (regs) return hxsLds(Rt, 0) <= 160 * 1024 && (GQ + 63) / 64 <= kHxsNP;
         const int dmas = (stageFor(G) / pieceBytes * dmaPerPiece + kHxsLoaders - 1) / kHxsLoaders;
         return hxsLds(Rt, stageFor(G)) <= 160 * 1024 && 2 * dmas <= 32 && 4 * ((GQ + 63) / 64 * 64) <= kHxsConvMax * nth;
     };
@@ -154,7 +159,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         break;
     }
     if (G == 0) return hipErrorNotSupported;
-    const int stageBytes = small ? 0 : stageFor(G);
+    const int stageBytes = (small || regs) ? 0 : stageFor(G);
 
     HxsArgs x{};
     x.A = static_cast<const h8v*>(p.A);
@@ -183,6 +188,11 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.fmt = fmt;
     x.stageBytes = stageBytes;
     x.small = small ? 1 : 0;
+    x.regs = regs ? 1 : 0;
+    static const int knobNt = std::getenv("GAR_HXS_NT") ? std::atoi(std::getenv("GAR_HXS_NT")) : 0;
+    static const int knobPair = std::getenv("GAR_HXS_PAIR") ? std::atoi(std::getenv("GAR_HXS_PAIR")) : 1;
+    x.nt = knobNt;
+    x.xcdPair = knobPair && fmt == 2 && (C / 16) % 2 == 0 && x.nblocks % 16 == 0 ? 1 : 0;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
     const int esz = od.f64 ? 8 : 4;
     x.out_f64 = od.f64;
@@ -208,8 +218,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.T1 = p.T1;
     x.T2 = p.T2;
     if (trace)
-        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
-                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
+        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d regs=%d fast[%lld,%lld)\n",
+                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst, x.regs,
                 (long long)x.fastLo, (long long)x.fastHi);
     const size_t lds = hxsLds(Rt, stageBytes);
     const int64_t blocks = x.nblocks;

@@ -32,6 +32,17 @@ namespace gar {
 constexpr int kHxsLoaders = 4;                          // loader waves per workgroup
 constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 waves per SIMD)
 constexpr int kHxsConvMax = 8;                          // staged items per thread per stage
+#ifdef GAR_HXS_DMA
+constexpr bool kHxsRegs = false;                        // A/B build: LDS-DMA raw-buffer pipeline, every wave converts
+#else
+constexpr bool kHxsRegs = true;                         // register staging (hxsRegLoaders)
+#endif
+#ifndef GAR_HXS_D
+#define GAR_HXS_D 2
+#define GAR_HXS_NP 7
+#endif
+constexpr int kHxsD = GAR_HXS_D;                        // register staging: loads in flight per loader wave
+constexpr int kHxsNP = GAR_HXS_NP;                      // register staging: 64-row pieces per load (G*Qc <= 64*NP)
 
 struct HxsArgs {
     const h8v* A;          // [nprog][NS][2][64] f16x8
@@ -46,6 +57,10 @@ struct HxsArgs {
     int stageBytes;        // raw LDS bytes of one stage (three buffers)
     int small;             // one period per column, window staged in one pass (hxsSmallStage)
     int vst, fmt;          // epilogue layout (template VST), raw stage layout 0 gathered ROW16 / 1 STEREO / 2 ROW16 DMA
+    int xcdPair;           // ROW16 blocks 2m, 2m+1 share every 128-B input/output line: run them on one XCD
+    int nt;                // development: non-temporal output stores (GAR_HXS_NT)
+    int regs;              // register staging (hxsRegLoaders): loaders load into VGPRs kHxsD loads ahead and
+                           // convert straight into the ring; compute waves only run MFMAs
     int64_t a_lo, a_hi;    // absolute macro periods of the launch
     int64_t o_lo, o_hi;    // outputs written
     const float* in;       // f32 input element (t, c) at in + t*in_fs + c*in_cs, t absolute, raw loads for t in [fastLo, fastHi)
@@ -84,6 +99,16 @@ __device__ __forceinline__ HxsArgsP hxsCold() {
     uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
     asm volatile("" : "+s"(v));
     return reinterpret_cast<HxsArgsP>(v);
+}
+
+// Logical block of launch slot i.  Workgroups are dispatched round-robin over the 8 XCDs (slot
+// i on XCD i % 8); with xcdPair, blocks 2m and 2m+1 -- the two halves of every 128-B line of
+// a ROW16 layout (16 channels x 4 B = 64 B per row) -- run as slots i and i + 8 on the same
+// XCD, so the second reader / writer of each line meets it in that XCD's L2.
+__device__ __forceinline__ int hxsBlock(const HxsArgs& x, int i) {
+    if (!x.xcdPair) return i;
+    const int s = i >> 3, xc = i & 7;
+    return ((s >> 1) * 8 + xc) * 2 + (s & 1);
 }
 
 // Exact value of output (a, r) of channel c (see hxExact in gar_hx.hpp).
@@ -177,6 +202,13 @@ __device__ __forceinline__ u32x4v hxsRsrc(const HxsArgs& x, int64_t row0, int64_
     r.z = __builtin_amdgcn_readfirstlane(nrec);
     r.w = 0x00020000u;
     return r;
+}
+
+// The same resource as a buffer-resource value (compiler-tracked raw_buffer_load builtins).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxsRsrcT(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
+    const u32x4v r = hxsRsrc(x, row0, cofs, elemBytes);
+    const uint64_t base = static_cast<uint64_t>(r.x) | (static_cast<uint64_t>(r.y) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, static_cast<int>(r.z), 0x00020000);
 }
 
 // One LDS-DMA piece: 64 lanes x 16 B from rsrc + voff (per lane) to LDS
@@ -404,6 +436,78 @@ __device__ __forceinline__ void hxsSmallStage(const HxsArgs& x, int b, int tid, 
     }
 }
 
+// ---- register staging (x.regs) ----------------------------------------------------
+// Loader wave q owns quad q (columns 4q..4q+3) of the block.  A load (rows
+// [T0, T0 + nrow) of the four columns) is kHxsNP pieces of 64 rows, lane l
+// holding row T0 + 64i + l of piece i as one f32x4 (the quad's four columns):
+//   STEREO  (fmt 1): chunks 2q, 2q+1, both channels -> two buffer_load_dwordx2
+//   ROW16   (fmt 2): channels 4q..4q+3 of one chunk  -> one buffer_load_dwordx4
+//   general (fmt 0): each column its own resource      -> four buffer_load_dword
+// Loads are issued kHxsD steps before their conversion (the compiler tracks
+// them: vmcnt waits only for the oldest), so about 3 x (G*Qc rows x 16 columns
+// x 4 B) per CU are in flight against HBM latency, and the raw data never
+// touches LDS.  Rows past the caller's input read zeros through the records.
+// Registers of one load, per format: STEREO two f2v per piece (chunks 2q, 2q+1), ROW16 one f32x4.
+// One loop per format (hxsRegLoadersT<FMT>), so a loaded register is never merged with another
+// format's value (a merge would be a copy, and a copy waits for the load).
+template <int FMT>
+struct HxsRegBuf {
+    f2v a[kHxsNP], b[kHxsNP];
+};
+template <>
+struct HxsRegBuf<2> {
+    f32x4 v[kHxsNP];
+};
+
+// Per-block load resources of loader wave q (fmt 1: chunks 2q, 2q+1; fmt 2: the block's chunk at
+// channel offset c0) and its lane's byte offset from row 0.
+struct HxsRegSrc {
+    __amdgpu_buffer_rsrc_t a, b;
+    int lane0, pieceB, rowB;  // lane's offset of row 0, bytes per 64-row piece, bytes per row
+};
+
+template <int FMT>
+__device__ __forceinline__ HxsRegSrc hxsRegSrc(const HxsArgs& x, int b, int q, int lane) {
+    HxsRegSrc r;
+    if (FMT == 1) {
+        const int k0 = (b * 16) >> 1;
+        r.a = hxsRsrcT(x, hxsChunkRow(x, k0 + 2 * q, 0), 0, 8);
+        r.b = hxsRsrcT(x, hxsChunkRow(x, k0 + 2 * q + 1, 0), 0, 8);
+        r.rowB = 8;
+        r.lane0 = lane * 8;
+    } else {
+        const int col0 = b * 16, k = col0 / x.C, c0 = col0 - k * x.C;
+        r.rowB = static_cast<int>(x.in_fs) * 4;
+        r.a = hxsRsrcT(x, hxsChunkRow(x, k, 0), c0, 64);
+        r.b = r.a;
+        r.lane0 = lane * r.rowB + 16 * q;
+    }
+    r.pieceB = 64 * r.rowB;
+    return r;
+}
+
+// Always kHxsNP pieces (x2 for STEREO) of load instructions, whatever the load: pieces it does not
+// need (past its rows, or a whole edge/absent load, `live` false) get an offset past every record,
+// which returns zeros without a memory access.  A fixed instruction pattern lets the compiler's
+// vmcnt tracking wait for exactly the oldest load; a conditional issue would make it wait for all.
+template <int FMT>
+__device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, HxsRegBuf<FMT>& r) {
+    const bool fast = FMT != 0 && live && st.fast;
+    const int npc = fast ? (st.nrow + 63) >> 6 : 0;
+    const int voff = st.T0 * rs.rowB + rs.lane0;
+#pragma unroll
+    for (int i = 0; i < kHxsNP; ++i) {
+        const int o = i < npc ? voff + rs.pieceB * i : static_cast<int>(0x80000000u);
+        if constexpr (FMT == 2) {
+            r.v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.a, o, 0, 0));
+        } else if constexpr (FMT == 1) {
+            r.a[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.a, o, 0, 0));
+            r.b[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.b, o, 0, 0));
+        }
+    }
+    return fast;
+}
+
 template <int VST>
 __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y, int lane) {
     if (VST == 2) {
@@ -414,12 +518,17 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
         f32x4 w;
         if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
         else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
-        *reinterpret_cast<f32x4*>(p) = w;
+        if (x.nt) __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
+        else *reinterpret_cast<f32x4*>(p) = w;
     } else if (VST == 1) {
-        *reinterpret_cast<f32x4*>(p) = y;
+        if (x.nt) __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(p));
+        else *reinterpret_cast<f32x4*>(p) = y;
     } else if (VST == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
+        for (int i = 0; i < 4; ++i) {
+            if (x.nt) __builtin_nontemporal_store(y[i], reinterpret_cast<float*>(p + i * x.out_fs));
+            else *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<double*>(p + i * x.out_fs) = static_cast<double>(y[i]);
@@ -432,6 +541,14 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
 //   step j = 0 .. P + ngroups - 1: every wave converts load j; loaders issue
 //   load j + 2 and wait load j + 1; compute waves run MFMA group j - P (when
 //   >= 0: stage 0 and stages 1 .. j - P are in the ring); B | [fixup]
+// Steps of a block (P stage-0 parts + ngroups groups), padded to a multiple of kHxsD under
+// register staging so the loaders' unrolled loop issues the same loads on every path.
+__device__ __forceinline__ int hxsStepsPad(const HxsArgs& x) {
+    const int GQ = x.G * x.Qc;
+    const int n = (x.small ? 0 : (x.Wg + GQ - 1) / GQ) + x.ngroups;
+    return kHxsRegs ? (n + kHxsD - 1) / kHxsD * kHxsD : n;
+}
+
 struct HxsShared {
     char* ring;
     uint32_t QS;
@@ -440,6 +557,40 @@ struct HxsShared {
     int* flag;
     char* raw;  // [3][stageBytes]
 };
+
+// Register staging: load `st` -> ring rows of quad q, from the registers of its
+// issue (fast) or gathered now (edge stages: history seam, partial blocks).
+template <int FMT>
+__device__ __forceinline__ void hxsRegConvert(const HxsArgs& x, const HxsStage& st, bool fast, const HxsRegBuf<FMT>& r,
+                                              int b, int q, int lane, const HxsShared& sh) {
+    const int p0 = uni(st.T0 % x.R);
+    const int npc = (st.nrow + 63) >> 6;
+    if (FMT != 0 && fast) {
+#pragma unroll
+        for (int i = 0; i < kHxsNP; ++i) {
+            const int row = 64 * i + lane;
+            if (i < npc && row < st.nrow) {
+                f32x4 e;
+                if constexpr (FMT == 2) e = r.v[i];
+                else e = f32x4{r.a[i].x, r.a[i].y, r.b[i].x, r.b[i].y};
+                hxsPutItem(x, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+            }
+        }
+        return;
+    }
+    const HxsArgsP xc = hxsCold();
+    const SrcDesc src = kload(&xc->src);
+    for (int row = lane; row < st.nrow; row += 64) {
+        f32x4 e;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int col = b * 16 + 4 * q + n;
+            const int k = col / x.C, c = col - k * x.C;
+            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + row), c, x.A) : 0.f;
+        }
+        hxsPutItem(x, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+    }
+}
 
 // Compute waves (one row block each).
 template <int NS, int VST>
@@ -466,7 +617,8 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
 
     const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
 
-    for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
+    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+        const int b = hxsBlock(x, bi);
         hxsBarrier();  // loud state reset; the previous block's ring reads done
         if (x.small) hxsSmallStage(x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
         hxsBarrier();  // load 0 landed (small: the whole window in the ring)
@@ -497,15 +649,16 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
                 }
             }
         };
-        for (int j = 0; j < P + x.ngroups; ++j) {
+        const int nstepsPad = hxsStepsPad(x);
+        for (int j = 0; j < nstepsPad; ++j) {
             // load j -> ring (this wave's share), then the MFMA periods of group j - P
             const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            if (j < nL && !((x.dbg & 16) && j >= P) && !((x.dbg & 32) && j >= P))
+            if (!kHxsRegs && j < nL && !((x.dbg & 16) && j >= P) && !((x.dbg & 32) && j >= P))
                 hxsConvert(x, hxsLoad(x, b, j, P), sh_.raw + (j % 3) * x.stageBytes, tid, nth, sh_.ring, QS,
                            sh_.loudLo, sh_.loudHi, sh_.flag);
             if (x.prof) tcv += __builtin_amdgcn_s_memtime() - t0;
             const int g = j - P;
-            if (g < 0) {
+            if (g < 0 || g >= x.ngroups) {
                 hxsBarrier();
                 continue;
             }
@@ -579,14 +732,81 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     }
 }
 
+// Register-staging loader wave q (x.regs): same barrier sequence as the compute
+// waves; in step j it converts load j (issued kHxsD steps earlier) into the ring
+// and issues load j + kHxsD into the registers just freed.
+template <int FMT>
+__device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared& sh_, int q, int lane) {
+    const int GQ = x.G * x.Qc;
+    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
+    const int nstepsPad = hxsStepsPad(x);
+    const int tid = (x.nprog + q) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    unsigned long long pc = 0, pi = 0, pb = 0;
+    const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+        const int b = hxsBlock(x, bi);
+        if (q == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
+        if (q == 0 && lane == 0) *sh_.flag = 0;
+        hxsBarrier();  // loud state reset; the previous block's ring reads done
+        HxsRegBuf<FMT> buf[kHxsD];
+        bool fastL[kHxsD];
+        const HxsRegSrc rs = hxsRegSrc<FMT>(x, b, q, lane);
+#pragma unroll
+        for (int d = 0; d < kHxsD; ++d) fastL[d] = hxsRegIssue<FMT>(hxsLoad(x, b, d, P), d < nL, rs, buf[d]);
+        if (x.small) hxsSmallStage(x, b, tid, nth, sh_.ring, sh_.QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        hxsBarrier();  // (small: the whole window in the ring)
+        for (int j0 = 0; j0 < nstepsPad; j0 += kHxsD) {
+#pragma unroll
+            for (int d = 0; d < kHxsD; ++d) {
+                const int j = j0 + d;
+                const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+                if (j < nL && !((x.dbg & 16) && j >= P))
+                    hxsRegConvert<FMT>(x, hxsLoad(x, b, j, P), fastL[d], buf[d], b, q, lane, sh_);
+                const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+                fastL[d] = hxsRegIssue<FMT>(hxsLoad(x, b, j + kHxsD, P), j + kHxsD < nL && !((x.dbg & 1) && j >= P), rs,
+                                            buf[d]);
+                const unsigned long long t2 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
+                hxsBarrier();  // step done: load j in the ring
+                if (x.prof) {
+                    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+                    pc += t1 - t0; pi += t2 - t1; pb += t3 - t2;
+                }
+            }
+        }
+        if (*sh_.flag) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
+        }
+    }
+    if (x.prof && lane == 0) {
+        atomicAdd(x.prof + 0, pc);
+        atomicAdd(x.prof + 1, pi);
+        atomicAdd(x.prof + 2, pb);
+        atomicAdd(x.prof + 3, 1ull);
+        atomicAdd(x.prof + 9, __builtin_amdgcn_s_memrealtime() - rStart);
+    }
+}
+
+__device__ __forceinline__ void hxsRegLoaders(const HxsArgs& x, const HxsShared& sh_, int q, int lane) {
+    if (x.fmt == 1) hxsRegLoadersT<1>(x, sh_, q, lane);
+    else if (x.fmt == 2) hxsRegLoadersT<2>(x, sh_, q, lane);
+    else hxsRegLoadersT<0>(x, sh_, q, lane);
+}
+
 // Loader waves: the DMAs (or gathers) of every stage, two groups ahead, and their share of the conversion.
 __device__ __forceinline__ void hxsLoaders(const HxsArgs& x, const HxsShared& sh_, int wl, int lane) {
+    if (kHxsRegs) {
+        hxsRegLoaders(x, sh_, wl, lane);
+        return;
+    }
     const int GQ = x.G * x.Qc;
     const int tid = (x.nprog + wl) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
     const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
     unsigned long long tc = 0, tl = 0, tb = 0, ti = 0, tpre = 0, tloop = 0;
     const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-    for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
+    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+        const int b = hxsBlock(x, bi);
         if (wl == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
         if (wl == 0 && lane == 0) *sh_.flag = 0;
         hxsBarrier();  // loud state reset; the previous block's ring reads done

@@ -30,7 +30,13 @@ def run(env):
     e = dict(os.environ, **{k: str(v) for k, v in env.items()})
     out = subprocess.run([sys.executable, "-c", CHILD], env=e, capture_output=True, text=True, timeout=300)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    return json.loads(line[-1]) if line else {"err": out.stderr[-500:]}
+    if not line:
+        return {"err": out.stderr[-500:]}
+    d = json.loads(line[-1])
+    prof = [l for l in out.stderr.splitlines() if l.startswith("hxs")]
+    if prof:
+        d["prof"] = prof
+    return d
 
 if __name__ == "__main__":
     configs = json.loads(sys.argv[1]) if len(sys.argv) > 1 else [{}]
