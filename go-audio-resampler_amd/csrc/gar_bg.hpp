@@ -21,6 +21,7 @@ __device__ __forceinline__ TC srcRead(const SrcDesc& s, int64_t t, int c) {
     const int64_t i = t - s.in_base;
     if (i >= 0 && i < s.in_len) {
         const int64_t e = i * s.in_fs + static_cast<int64_t>(c) * s.in_cs;
+        if (s.in_pcm) return static_cast<TC>(pcmRead(s.in, e, s.in_pcm));
         return s.in_f64 ? static_cast<TC>(static_cast<const double*>(s.in)[e])
                         : static_cast<TC>(static_cast<const float*>(s.in)[e]);
     }
@@ -31,7 +32,8 @@ template <class TC>
 __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, TC v) {
     if (idx < o.o_lo || idx >= o.o_hi) return;
     const int64_t e = (idx - o.o0) * o.fs + static_cast<int64_t>(c) * o.cs;
-    if (o.f64) static_cast<double*>(o.out)[e] = static_cast<double>(v);
+    if (o.pcm) pcmWrite(o.out, e, o.pcm, static_cast<double>(v));
+    else if (o.f64) static_cast<double*>(o.out)[e] = static_cast<double>(v);
     else static_cast<float*>(o.out)[e] = static_cast<float>(v);
 }
 
@@ -146,7 +148,7 @@ __device__ __forceinline__ ColSrc<TC> colSrc(const SrcDesc& s, const BgGrid& g, 
     r.p = nullptr;
     r.stride = 0;
     const int64_t t1 = r.t0 + g.W;
-    const bool inSame = (s.in_f64 != 0) == (sizeof(TC) == 8);
+    const bool inSame = !s.in_pcm && (s.in_f64 != 0) == (sizeof(TC) == 8);
     if (r.ok && t1 <= s.valid_end) {
         if (inSame && s.in && r.t0 >= s.in_base && t1 <= s.in_base + s.in_len) {
             r.p = static_cast<const TC*>(s.in) + (r.t0 - s.in_base) * s.in_fs + static_cast<int64_t>(r.c) * s.in_cs;

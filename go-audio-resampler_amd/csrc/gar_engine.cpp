@@ -331,6 +331,7 @@ struct InView {
     const void* p = nullptr;
     int64_t fs = 0, cs = 0;
     int f64 = 0;
+    int pcm = 0;  // integer PCM input bits (fused into hxs_kernel's loads; gar_process_device only)
     int64_t n = 0;
     bool zeros = false;
 };
@@ -339,6 +340,7 @@ struct OutView {
     void* p = nullptr;
     int64_t fs = 0, cs = 0;
     int f64 = 0;
+    int pcm = 0;  // integer PCM output bits (fused into hxs_kernel's stores)
 };
 
 // Pinned host buffer the device reads in place (CubicStage checkpoints); reused only
@@ -457,8 +459,9 @@ hipError_t timed(Ctx& x, int tag, L&& launch) {
         b = x.h->evPool.back().second;
         x.h->evPool.pop_back();
     } else {
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
+        // timing only: no system-scope fence (it would add an L2 writeback to the timed launch)
+        HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+        HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
     }
     HIPCHK(hipEventRecord(a, x.s));
     const hipError_t e = launch();
@@ -483,6 +486,7 @@ SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
     s.in_fs = in.fs;
     s.in_cs = in.cs;
     s.in_f64 = in.f64;
+    s.in_pcm = in.zeros ? 0 : in.pcm;
     s.valid_end = in.zeros ? x0 : x0 + in.n;
     return s;
 }
@@ -494,6 +498,7 @@ OutDesc mkOut(const OutView& o, int64_t o0, int64_t n) {
     d.fs = o.fs;
     d.cs = o.cs;
     d.f64 = o.f64;
+    d.pcm = o.pcm;
     d.o_lo = o0;
     d.o_hi = o0 + n;
     return d;
@@ -730,7 +735,7 @@ int64_t stageFlush(Ctx& x, int si, const OutView& out) {
 
 OutView offsetView(const OutView& o, int64_t rows) {
     OutView r = o;
-    if (o.p) r.p = static_cast<char*>(o.p) + rows * o.fs * (o.f64 ? 8 : 4);
+    if (o.p) r.p = static_cast<char*>(o.p) + rows * o.fs * (o.pcm ? pcmBytes(o.pcm) : (o.f64 ? 8 : 4));
     return r;
 }
 
@@ -992,7 +997,10 @@ gar_status initDevice(Handle* h) {
     }
     HIPCHK(hipSetDevice(h->device));
     HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&h->orderEv, hipEventDisableTiming));
+    // device-scope release: the event only orders this handle's calls across streams of its
+    // device (host visibility of results goes through the stream syncs of the host paths); a
+    // system-scope release would write back every dirty L2 line after each call
+    HIPCHK(hipEventCreateWithFlags(&h->orderEv, hipEventDisableTiming | hipEventDisableSystemFence));
     return GAR_OK;
 }
 
@@ -1132,6 +1140,22 @@ gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t c
     });
 }
 
+}  // namespace
+}  // namespace gar
+
+namespace gar {
+namespace {
+bool isPcm(int32_t t) { return t == GAR_PCM16 || t == GAR_PCM24 || t == GAR_PCM32; }
+bool ioTypeOk(int32_t t) { return t == GAR_F64 || t == GAR_F32 || t == GAR_F32_EXACT || isPcm(t); }
+// PCM conversion fused into hxs_kernel's loads and stores: one fused split-f16 stage streaming
+// through the row-block kernel (launchHxs's geometry); anything else stages the conversion.
+bool pcmFusable(const Handle* h) {
+    if (h->dry || h->f64 || !h->hx || h->stages.size() != 1 || h->groups.size() != 1) return false;
+    const StageRT& st = *h->stages[0];
+    if (!st.fused || h->groups[0].cnt.empty() || h->groups[0].cnt[0].staged) return false;
+    const HxDev* hx = st.fusedD.hx;
+    return hx && hx->rb && hx->nw <= kHxRbMaxWaves && hx->NS >= 1 && hx->NS <= 10;
+}
 }  // namespace
 }  // namespace gar
 
@@ -1341,22 +1365,56 @@ gar_status gar_process_device(gar_resampler* r, const void* in, int32_t in_dtype
     }
     if (frames < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
     if (frames > 0 && !in) return guard(GAR_ERR_INVALID_ARGUMENT, "input is NULL");
+    if (!ioTypeOk(in_dtype) || !ioTypeOk(out_dtype)) return guard(GAR_ERR_INVALID_ARGUMENT, "unknown sample type");
     if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep (per-channel calls were made)");
     return callOn(r, static_cast<hipStream_t>(stream), [&]() -> gar_status {
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
+        const bool fuse = pcmFusable(r);
         InView iv;
         iv.p = in;
         iv.f64 = in_dtype == GAR_F64 ? 1 : 0;
         iv.fs = in_fs;
         iv.cs = in_cs;
         iv.n = frames;
+        if (isPcm(in_dtype)) {
+            iv.f64 = 0;
+            if (fuse) {
+                iv.pcm = in_dtype;
+            } else if (!r->dry) {  // staged: PCM -> compute dtype, then the ordinary path
+                const int cf = r->f64 ? 1 : 0;
+                r->inStage.ensure(static_cast<size_t>(std::max<int64_t>(frames, 1)) * r->channels * (cf ? 8 : 4));
+                HIPCHK(launchConvert(in, in_dtype, in_fs, in_cs, r->inStage.p, cf, r->channels, 1, frames, r->channels, s));
+                iv.p = r->inStage.p;
+                iv.f64 = cf;
+                iv.fs = r->channels;
+                iv.cs = 1;
+            }
+        }
         OutView ov;
         ov.p = out;
         ov.f64 = out_dtype == GAR_F64 ? 1 : 0;
         ov.fs = out_fs;
         ov.cs = out_cs;
+        const bool stageOut = isPcm(out_dtype) && !fuse && !r->dry;
+        if (isPcm(out_dtype)) {
+            ov.f64 = 0;
+            if (fuse) ov.pcm = out_dtype;
+        }
+        if (stageOut) {
+            std::vector<int64_t> sz;
+            const int64_t need = simulate(r, r->groups[0], frames, false, sz);
+            const int cf = r->f64 ? 1 : 0;
+            r->outStage.ensure(static_cast<size_t>(std::max<int64_t>(need, 1)) * r->channels * (cf ? 8 : 4));
+            ov.p = r->outStage.p;
+            ov.f64 = cf;
+            ov.fs = r->channels;
+            ov.cs = 1;
+        }
         gar_status st;
-        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
         const int64_t got = runGroup(r, r->groups[0], iv, ov, false, s, out_cap, st);
+        if (st == GAR_OK && stageOut && got > 0)
+            HIPCHK(launchConvert(r->outStage.p, r->f64 ? 1 : 0, r->channels, 1, out, out_dtype, out_fs, out_cs, got,
+                                 r->channels, s));
         if (st == GAR_OK && out_frames) *out_frames = got;
         return st;
     });
@@ -1370,16 +1428,36 @@ gar_status gar_flush_device(gar_resampler* r, int32_t channels, void* out, int32
         g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(channels);
         return GAR_ERR_CHANNEL_MISMATCH;
     }
+    if (!ioTypeOk(out_dtype)) return guard(GAR_ERR_INVALID_ARGUMENT, "unknown sample type");
     if (r->groups.size() != 1) return guard(GAR_ERR_NOT_SUPPORTED, "channels are not in lockstep");
     return callOn(r, static_cast<hipStream_t>(stream), [&]() -> gar_status {
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
+        const bool fuse = pcmFusable(r);
         OutView ov;
         ov.p = out;
         ov.f64 = out_dtype == GAR_F64 ? 1 : 0;
         ov.fs = out_fs;
         ov.cs = out_cs;
+        const bool stageOut = isPcm(out_dtype) && !fuse && !r->dry;
+        if (isPcm(out_dtype)) {
+            ov.f64 = 0;
+            if (fuse) ov.pcm = out_dtype;
+        }
+        if (stageOut) {
+            std::vector<int64_t> sz;
+            const int64_t need = simulate(r, r->groups[0], 0, true, sz);
+            const int cf = r->f64 ? 1 : 0;
+            r->outStage.ensure(static_cast<size_t>(std::max<int64_t>(need, 1)) * r->channels * (cf ? 8 : 4));
+            ov.p = r->outStage.p;
+            ov.f64 = cf;
+            ov.fs = r->channels;
+            ov.cs = 1;
+        }
         gar_status st;
-        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = legacy default stream
         const int64_t got = runGroup(r, r->groups[0], InView(), ov, true, s, out_cap, st);
+        if (st == GAR_OK && stageOut && got > 0)
+            HIPCHK(launchConvert(r->outStage.p, r->f64 ? 1 : 0, r->channels, 1, out, out_dtype, out_fs, out_cs, got,
+                                 r->channels, s));
         if (st == GAR_OK && out_frames) *out_frames = got;
         return st;
     });

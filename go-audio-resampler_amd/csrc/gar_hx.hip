@@ -44,6 +44,7 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
         const hipError_t e = launchHxs(p, src, od, C, stream);
         if (e != hipErrorNotSupported) return e;
     }
+    if (od.pcm) return hipErrorNotSupported;  // PCM output is fused into hxs_kernel only (engine stages it otherwise)
     // development knobs: GAR_HX_G caps macro periods per column; GAR_HX_DBG bits: 1 skip
     // staging after the first block, 2 skip the MFMA programs, 16 skip the loop
     static const int knobG = std::getenv("GAR_HX_G") ? std::atoi(std::getenv("GAR_HX_G")) : 0;
@@ -78,7 +79,7 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
     // interior chunks [k0, k1): outputs inside [o_lo, o_hi), window rows [0, W) inside the f32 input,
     // and 32-bit lane offsets (row * frame stride) inside a buffer resource
     int64_t k0 = 0, k1 = 0;
-    const bool fastIn = src.in && !src.in_f64 && src.in_len > 0 &&
+    const bool fastIn = src.in && !src.in_f64 && !src.in_pcm && src.in_len > 0 &&
                         static_cast<double>(wsFor(G)) * static_cast<double>(std::llabs(src.in_fs)) * 4.0 < 2147483647.0 &&
                         src.in_fs > 0 && src.in_cs >= 0;
     if (fastIn) {

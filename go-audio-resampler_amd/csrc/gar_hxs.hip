@@ -79,11 +79,8 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 }
 }  // namespace
 
-// LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B),
-// three raw stage buffers.
-static size_t hxsLds(int Rt, int stageBytes) {
-    return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256 + 3 * static_cast<size_t>(stageBytes);
-}
+// LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B).
+static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256; }
 
 // hipErrorNotSupported: the plan does not fit this kernel's geometry (the caller uses hx_kernel).
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
@@ -111,8 +108,10 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     if (knobNp > 0 && !small) Np = knobNp;  // development: chunk length in macro periods
     // raw loads address a chunk's rows with 32-bit offsets from the chunk's first row:
     // (Np*Qc + rows of one group + a piece) rows must span less than 2^31 bytes
-    const int64_t rowBytes = std::max<int64_t>(4, src.in_fs * 4);
-    const int64_t npMax = ((int64_t(1) << 31) / rowBytes - (3 * Qc + p.Kread + 256)) / Qc;
+    const int inEsz = src.in_pcm ? pcmBytes(src.in_pcm) : (src.in_f64 ? 8 : 4);
+    const int64_t rowBytes = std::max<int64_t>(4, src.in_fs * inEsz);
+    const int64_t chunksPerRsrc = (C <= 16 && 16 % C == 0) ? 16 / C : 1;  // STEREO: one resource spans 8 chunks
+    const int64_t npMax = ((int64_t(1) << 31) / rowBytes / chunksPerRsrc - (3 * Qc + p.Kread + 256)) / Qc;
     const bool rawSpan = npMax >= 1;
     if (rawSpan) Np = std::min(Np, npMax);
     int64_t nchunk = cdiv(nmac, Np);
@@ -131,22 +130,24 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         // the four quads of a transposed read land on distinct banks
         Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
     };
-    // raw stage layout: STEREO pieces (128 rows x 8 chunks, LDS-DMA dwordx4), ROW16 pieces (16 rows x 16
-    // channels, LDS-DMA dwordx4) or gathered ROW16 pieces for any other layout
+    // load layout: STEREO frames (two chunks per quad, dwordx2), ROW16 (four channels per quad,
+    // dwordx4), or gathered at conversion time for any other layout
     const uintptr_t inA = reinterpret_cast<uintptr_t>(src.in);
     int fmt = 0;
-    if ((inA & 7) == 0 && C == 2 && src.in_fs == 2 && src.in_cs == 1) fmt = 1;
-    else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) fmt = 2;
-    const int RPc = fmt == 1 ? 128 : 16, pieceBytes = fmt == 1 ? 8192 : 1024, dmaPerPiece = fmt == 1 ? 8 : 1;
-    auto stageFor = [&](int G) { return (G * static_cast<int>(Qc) + RPc - 1) / RPc * pieceBytes; };
-    const int nth = 64 * (p.nw + kHxsLoaders);
-    // register staging (default; -DGAR_HXS_DMA builds the LDS-DMA raw-buffer pipeline)
-    const bool regs = kHxsRegs && !small;
+    const bool stereoIl = C == 2 && src.in_fs == 2 && src.in_cs == 1;
+    if (src.in_pcm == 16) {  // PCM16 / PCM24-32 stereo frames; other PCM layouts are gathered
+        if ((inA & 3) == 0 && stereoIl) fmt = 3;
+    } else if (src.in_pcm) {
+        if ((inA & 7) == 0 && stereoIl) fmt = 4;
+    } else if (src.in_f64) {
+    } else if ((inA & 7) == 0 && stereoIl) {
+        fmt = 1;
+    } else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) {
+        fmt = 2;
+    }
     auto fits = [&](int G, int Rt) {
         const int GQ = G * static_cast<int>(Qc);
-        if (regs) return hxsLds(Rt, 0) <= 160 * 1024 && (GQ + 63) / 64 <= kHxsNP;
-        const int dmas = (stageFor(G) / pieceBytes * dmaPerPiece + kHxsLoaders - 1) / kHxsLoaders;
-        return hxsLds(Rt, stageFor(G)) <= 160 * 1024 && 2 * dmas <= 32 && 4 * ((GQ + 63) / 64 * 64) <= kHxsConvMax * nth;
+        return hxsLds(Rt) <= 160 * 1024 && (GQ + 63) / 64 <= kHxsNP;
     };
     int G = 0, R = 0, Rt = 0, Wg = 0;
     for (int cand = small ? 1 : 3; cand >= 1; --cand) {
@@ -159,7 +160,6 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         break;
     }
     if (G == 0) return hipErrorNotSupported;
-    const int stageBytes = (small || regs) ? 0 : stageFor(G);
 
     HxsArgs x{};
     x.A = static_cast<const h8v*>(p.A);
@@ -178,29 +178,31 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.o_lo = od.o_lo; x.o_hi = od.o_hi;
     // raw input: element (t, c) at in + t*in_fs + c*in_cs for t in [fastLo, fastHi) (integer arithmetic:
     // the base may point outside the caller's buffer, only rows inside it are dereferenced)
-    const bool rawOk = src.in && !src.in_f64 && src.in_len > 0 && src.in_fs > 0 && src.in_cs >= 0 && rawSpan;
-    x.in = reinterpret_cast<const float*>(reinterpret_cast<uintptr_t>(src.in) -
-                                          static_cast<uintptr_t>(src.in_base * src.in_fs * 4));
+    const bool rawOk = src.in && fmt != 0 && src.in_len > 0 && src.in_fs > 0 && src.in_cs >= 0 && rawSpan;
+    x.in_esz = inEsz;
+    x.in_pcm = src.in_pcm;
+    x.in = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(src.in) -
+                                         static_cast<uintptr_t>(src.in_base * src.in_fs * inEsz));
     x.in_fs = src.in_fs;
     x.in_cs = src.in_cs;
     x.fastLo = rawOk ? src.in_base : 0;
     x.fastHi = rawOk ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
     x.fmt = fmt;
-    x.stageBytes = stageBytes;
     x.small = small ? 1 : 0;
-    x.regs = regs ? 1 : 0;
     static const int knobNt = std::getenv("GAR_HXS_NT") ? std::atoi(std::getenv("GAR_HXS_NT")) : 0;
     static const int knobPair = std::getenv("GAR_HXS_PAIR") ? std::atoi(std::getenv("GAR_HXS_PAIR")) : 1;
     x.nt = knobNt;
     x.xcdPair = knobPair && fmt == 2 && (C / 16) % 2 == 0 && x.nblocks % 16 == 0 ? 1 : 0;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
-    const int esz = od.f64 ? 8 : 4;
+    const int esz = od.pcm ? pcmBytes(od.pcm) : (od.f64 ? 8 : 4);
+    x.out_pcm = od.pcm;
     x.out_f64 = od.f64;
     x.out = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(od.out) - static_cast<uintptr_t>(od.o0 * od.fs * esz));
     x.out_fs = od.fs * esz;
     x.out_cs = od.cs * esz;
     const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
-    if (od.f64) x.vst = 3;
+    if (od.pcm) x.vst = 0;  // PCM stores: the epilogue's checked per-element path
+    else if (od.f64) x.vst = 3;
     else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;
     else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;
     else x.vst = 0;
@@ -218,10 +220,10 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.T1 = p.T1;
     x.T2 = p.T2;
     if (trace)
-        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d regs=%d fast[%lld,%lld)\n",
-                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst, x.regs,
+        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
+                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
                 (long long)x.fastLo, (long long)x.fastHi);
-    const size_t lds = hxsLds(Rt, stageBytes);
+    const size_t lds = hxsLds(Rt);
     const int64_t blocks = x.nblocks;
     switch (p.NS) {
 #define GAR_HXS_NS(n) case n: return hxsVst<n>(x, lds, blocks, stream);

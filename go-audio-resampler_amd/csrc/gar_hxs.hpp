@@ -29,20 +29,17 @@
 
 namespace gar {
 
-constexpr int kHxsLoaders = 4;                          // loader waves per workgroup
-constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 waves per SIMD)
-constexpr int kHxsConvMax = 8;                          // staged items per thread per stage
-#ifdef GAR_HXS_DMA
-constexpr bool kHxsRegs = false;                        // A/B build: LDS-DMA raw-buffer pipeline, every wave converts
-#else
-constexpr bool kHxsRegs = true;                         // register staging (hxsRegLoaders)
+#ifndef GAR_HXS_L
+#define GAR_HXS_L 6
 #endif
+constexpr int kHxsLoaders = GAR_HXS_L;                  // loader waves per workgroup
+constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 waves per SIMD, 128 VGPRs)
 #ifndef GAR_HXS_D
-#define GAR_HXS_D 2
-#define GAR_HXS_NP 7
+#define GAR_HXS_D 3
 #endif
-constexpr int kHxsD = GAR_HXS_D;                        // register staging: loads in flight per loader wave
-constexpr int kHxsNP = GAR_HXS_NP;                      // register staging: 64-row pieces per load (G*Qc <= 64*NP)
+constexpr int kHxsD = GAR_HXS_D;                        // loads in flight per loader wave (register staging)
+constexpr int kHxsNP = 7;                               // 64-row pieces per load (G*Qc <= 448)
+constexpr int kHxsItems = (4 * kHxsNP + kHxsLoaders - 1) / kHxsLoaders;  // (quad, piece) items per loader per load
 
 struct HxsArgs {
     const h8v* A;          // [nprog][NS][2][64] f16x8
@@ -54,17 +51,16 @@ struct HxsArgs {
     unsigned long long* prof;  // development: per-phase cycle sums (GAR_HXS_PROF), null in production
     int dbg;               // development attribution (GAR_HXS_DBG, wrong output): 1 no steady DMAs, 2 no stores,
                            // 4 no MFMA, 16 no steady conversion
-    int stageBytes;        // raw LDS bytes of one stage (three buffers)
     int small;             // one period per column, window staged in one pass (hxsSmallStage)
-    int vst, fmt;          // epilogue layout (template VST), raw stage layout 0 gathered ROW16 / 1 STEREO / 2 ROW16 DMA
+    int vst, fmt;          // epilogue layout (template VST), load layout 0 gathered / 1 STEREO / 2 ROW16
     int xcdPair;           // ROW16 blocks 2m, 2m+1 share every 128-B input/output line: run them on one XCD
     int nt;                // development: non-temporal output stores (GAR_HXS_NT)
-    int regs;              // register staging (hxsRegLoaders): loaders load into VGPRs kHxsD loads ahead and
-                           // convert straight into the ring; compute waves only run MFMAs
     int64_t a_lo, a_hi;    // absolute macro periods of the launch
     int64_t o_lo, o_hi;    // outputs written
-    const float* in;       // f32 input element (t, c) at in + t*in_fs + c*in_cs, t absolute, raw loads for t in [fastLo, fastHi)
+    const char* in;        // input element (t, c) at byte in + (t*in_fs + c*in_cs)*in_esz, t absolute, raw loads for t in [fastLo, fastHi)
     int64_t in_fs, in_cs, fastLo, fastHi;
+    int in_esz, in_pcm;    // bytes per input element; PCM bits (0: float input)
+    int out_pcm;           // PCM output bits (0: float output; stores go through the checked path)
     char* out;             // output (o, c) at out + o*out_fs + c*out_cs (bytes), o absolute
     int64_t out_fs, out_cs;
     int out_f64;
@@ -168,33 +164,30 @@ __device__ __forceinline__ void hxsFixup(HxsArgsP xp, int b, const int* loudLo, 
 }
 
 // ---- staging --------------------------------------------------------------------
-// A stage (rows [T0, T0 + nrow) of every column of the block) travels:
-//   global --LDS-DMA (loader waves)--> raw buffer --split (every wave)--> ring.
-// Stage k is needed by group k; it is DMA'd during group k-2 into raw buffer
-// k % 3, the loaders' vmcnt wait before the end of group k-1 makes it visible
-// to every wave, and during group k-1 all waves convert their share of it.
-// Raw layouts:
-//  * STEREO (fmt 1, C == 2): pieces of 128 rows x the 8 chunks of the block,
-//    [piece][chunk][row][2 channels]; one buffer_load_dwordx4 ... lds per
-//    (piece, chunk) (64 lanes = 128 frames, 1 KiB contiguous).
-//  * ROW16 (fmt 2 with C % 16 == 0: the 16 columns are 16 channels of one
-//    chunk): pieces of 16 rows, [piece][row][16]; one buffer_load_dwordx4 ...
-//    lds per piece (lane = (row, quad)).
-//  * every other layout: ROW16 pieces gathered through registers.
-// Rows past the caller's input read zeros through the buffer records; rows
-// before it (history seam, stream start) are gathered.
+// A load (rows [T0, T0 + nrow) of every column of the block) travels:
+//   global --buffer loads (loader waves, kHxsD loads ahead)--> VGPRs --f16 hi/lo split--> ring.
+// A load is 4 quads x kHxsNP pieces of 64 rows; loader wave l owns the (quad, piece) items
+// l, l + kHxsLoaders, ... (item = 4 * piece + quad), lane = row of the piece.  Layouts:
+//  * STEREO (fmt 1, C == 2, frames interleaved): quad q = chunks 2q, 2q+1 (two channels each),
+//    one buffer_load_dwordx2 per chunk (64 lanes = 512 B contiguous);
+//  * ROW16 (fmt 2, C % 16 == 0, 16-B aligned rows): quad q = channels 4q..4q+3 of the block's
+//    chunk, one buffer_load_dwordx4;
+//  * every other layout, f64 input and the edges (rows before the input: history seam, stream
+//    start; partial blocks): gathered at conversion time.
+// Rows past the caller's input read zeros through the buffer records.
 struct HxsStage {
     int T0, nrow;   // column-relative first row and row count
-    bool fast;      // LDS-DMA: every column live, no row before the raw f32 input
+    bool fast;      // buffer loads: every column live, no row before the raw f32 input
 };
 
 // Buffer resource (raw, stride 0) over the raw input from absolute row `row0`
 // of channel offset `cofs` (elements): records end at row fastHi, so loads past
 // the caller's input (the tail of the last chunk) read zeros.
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4v hxsRsrc(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
-    const uint64_t base = reinterpret_cast<uint64_t>(x.in + row0 * x.in_fs + cofs);
-    const int64_t nb = x.fastHi > row0 ? (x.fastHi - row0 - 1) * x.in_fs * 4 + elemBytes : 0;
+template <class XP>
+__device__ __forceinline__ u32x4v hxsRsrc(XP x, int64_t row0, int64_t cofs, int elemBytes) {
+    const uint64_t base = reinterpret_cast<uint64_t>(x->in + (row0 * x->in_fs + cofs) * x->in_esz);
+    const int64_t nb = x->fastHi > row0 ? (x->fastHi - row0 - 1) * x->in_fs * x->in_esz + elemBytes : 0;
     const unsigned nrec = static_cast<unsigned>(nb < 0x7fffffff ? nb : 0x7fffffff);
     u32x4v r;
     r.x = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(base));
@@ -205,26 +198,11 @@ __device__ __forceinline__ u32x4v hxsRsrc(const HxsArgs& x, int64_t row0, int64_
 }
 
 // The same resource as a buffer-resource value (compiler-tracked raw_buffer_load builtins).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxsRsrcT(const HxsArgs& x, int64_t row0, int64_t cofs, int elemBytes) {
+template <class XP>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hxsRsrcT(XP x, int64_t row0, int64_t cofs, int elemBytes) {
     const u32x4v r = hxsRsrc(x, row0, cofs, elemBytes);
     const uint64_t base = static_cast<uint64_t>(r.x) | (static_cast<uint64_t>(r.y) << 32);
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, static_cast<int>(r.z), 0x00020000);
-}
-
-// One LDS-DMA piece: 64 lanes x 16 B from rsrc + voff (per lane) to LDS
-// [lds, lds + 1 KiB), lane-linear.  Inline asm on purpose: the compiler then
-// does not track the piece as a pending LDS write, so it inserts no vmcnt(0)
-// before every later LDS access of the wave (the conversion's ring writes);
-// the pieces are waited for explicitly (hxsWaitVm) before the barrier that
-// publishes them.
-__device__ __forceinline__ void hxsDma16(u32x4v rs, const void* lds, int voff) {
-    const unsigned a = __builtin_amdgcn_readfirstlane(
-        static_cast<unsigned>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)lds)));
-    unsigned m0save;  // m0 is reserved to the compiler: restored after the issue
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(m0save)
-                 : "v"(voff), "s"(rs), "s"(a)
-                 : "memory");
 }
 
 // Element (t, c) of the stream for edge stages: history | input (f32/f64) |
@@ -236,6 +214,12 @@ __device__ __forceinline__ float hxsGather(const SrcDesc& s, int64_t t, int c, c
     const bool inH = valid && s.hist && h >= 0 && h < s.hist_len;
     const bool inI = valid && !inH && s.in && i >= 0 && i < s.in_len;
     const float* hp = static_cast<const float*>(s.hist) + (inH ? h * s.hist_ld + c : 0);
+    if (s.in_pcm) {  // integer PCM input (main.go:444-472 scaling)
+        const int64_t e = inI ? i * s.in_fs + static_cast<int64_t>(c) * s.in_cs : 0;
+        const float vh = *(inH ? hp : static_cast<const float*>(dummy));
+        const float vi = inI ? static_cast<float>(pcmRead(s.in, e, s.in_pcm)) : 0.f;
+        return inH ? vh : vi;
+    }
     if (s.in_f64) {
         const double* ip = static_cast<const double*>(s.in) + (inI ? i * s.in_fs + static_cast<int64_t>(c) * s.in_cs : 0);
         const float vh = *(inH ? hp : static_cast<const float*>(dummy));
@@ -247,114 +231,39 @@ __device__ __forceinline__ float hxsGather(const SrcDesc& s, int64_t t, int c, c
     return (inH || inI) ? v : 0.f;
 }
 
-__device__ __forceinline__ int64_t hxsChunkRow(const HxsArgs& x, int k, int T0) {
-    return (x.a_lo + static_cast<int64_t>(k) * x.Np) * x.Qc + T0;
+template <class XP>
+__device__ __forceinline__ int64_t hxsChunkRow(XP x, int k, int T0) {
+    return (x->a_lo + static_cast<int64_t>(k) * x->Np) * x->Qc + T0;
 }
 
 // Stage k of a block: k = 0 rows [0, Wg) (in parts of at most G*Qc), k >= 1
 // rows [Wg + (k-1)*G*Qc, Wg + k*G*Qc).
-__device__ __forceinline__ HxsStage hxsStage(const HxsArgs& x, int b, int T0, int nrow) {
+template <class XP>
+__device__ __forceinline__ HxsStage hxsStage(XP x, int b, int T0, int nrow) {
     HxsStage s;
     s.T0 = T0;
     s.nrow = nrow;
     const int c0 = b * 16, c1 = c0 + 15;
-    const int64_t tlo = (x.a_lo + static_cast<int64_t>(c0 / x.C) * x.Np) * x.Qc + T0;
-    s.fast = (x.fmt == 1 || x.fmt == 2) && c1 < x.ncols && tlo >= x.fastLo && x.fastHi > x.fastLo;
+    const int64_t tlo = (x->a_lo + static_cast<int64_t>(c0 / x->C) * x->Np) * x->Qc + T0;
+    s.fast = x->fmt >= 1 && x->fmt <= 4 && c1 < x->ncols && tlo >= x->fastLo && x->fastHi > x->fastLo;
     return s;
 }
 // Load j of a block: j < P = ceil(Wg / GQ) the parts of stage 0 (rows [j*GQ, ...) up to Wg),
 // then stage j - P + 1 (rows [Wg + (j-P)*GQ, + GQ)).
-__device__ __forceinline__ HxsStage hxsLoad(const HxsArgs& x, int b, int j, int P) {
-    const int GQ = x.G * x.Qc;
-    if (j < P) return hxsStage(x, b, j * GQ, min(GQ, x.Wg - j * GQ));
-    return hxsStage(x, b, x.Wg + (j - P) * GQ, GQ);
-}
-
-// Loader wave wl: DMA (fast) or gather (edge) its share of a stage into raw
-// buffer `raw`; returns the number of LDS-DMA instructions it issued.
-__device__ __forceinline__ int hxsIssue(const HxsArgs& x, const HxsStage& st, int b, int wl, int lane, char* raw) {
-    if (x.fmt == 1) {
-        const int npc = (st.nrow + 127) >> 7;
-        const int k0 = (b * 16) >> 1;  // first chunk of the block
-        if (st.fast) {
-            // this loader's two chunks (wl, wl + 4): one resource each from the chunk's row 0, the
-            // stage's rows as a per-lane offset (in range: Np*Qc + Wg rows fit 31 bits, launcher)
-            const u32x4v rA = hxsRsrc(x, hxsChunkRow(x, k0 + wl, 0), 0, 8);
-            const u32x4v rB = hxsRsrc(x, hxsChunkRow(x, k0 + wl + 4, 0), 0, 8);
-            const int rowB = static_cast<int>(x.in_fs) * 4;
-            int voff = st.T0 * rowB + lane * 16;
-            char* dst = raw + wl * 1024;
-            for (int pc = 0; pc < npc; ++pc) {
-                hxsDma16(rA, dst, voff);
-                hxsDma16(rB, dst + 4096, voff);
-                voff += 128 * rowB;
-                dst += 8192;
-            }
-            return 2 * npc;
-        }
-        const HxsArgsP xc = hxsCold();
-        const SrcDesc src = kload(&xc->src);
-        for (int d = wl; d < npc * 8; d += kHxsLoaders) {
-            const int pc = d >> 3, k = d & 7;
-            f32x4 e = {0.f, 0.f, 0.f, 0.f};
-            if (b * 16 + 2 * k < x.ncols) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    e[i] = hxsGather(src, hxsChunkRow(x, k0 + k, st.T0 + pc * 128 + (i >> 1) * 64 + lane), i & 1, x.A);
-            }
-            *reinterpret_cast<f2v*>(raw + d * 1024 + lane * 8) = f2v{e[0], e[1]};
-            *reinterpret_cast<f2v*>(raw + d * 1024 + 512 + lane * 8) = f2v{e[2], e[3]};
-        }
-        return 0;
-    }
-    const int npc = (st.nrow + 15) >> 4;
-    if (st.fast) {  // fmt 2: 16 channels of one chunk
-        const int col0 = b * 16, k = col0 / x.C, c0 = col0 - k * x.C;
-        const int fsB = static_cast<int>(x.in_fs) * 4;
-        const u32x4v rs = hxsRsrc(x, hxsChunkRow(x, k, 0), c0, 64);
-        int voff = (st.T0 + wl * 16 + (lane >> 2)) * fsB + (lane & 3) * 16;
-        int nd = 0;
-        for (int pc = wl; pc < npc; pc += kHxsLoaders) {
-            hxsDma16(rs, raw + pc * 1024, voff);
-            voff += kHxsLoaders * 16 * fsB;
-            ++nd;
-        }
-        return nd;
-    }
-    const HxsArgsP xc = hxsCold();
-    const SrcDesc src = kload(&xc->src);
-    for (int pc = wl; pc < npc; pc += kHxsLoaders) {
-        f32x4 e;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int col = b * 16 + 4 * (lane & 3) + n;
-            const int k = col / x.C, c = col - k * x.C;
-            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + pc * 16 + (lane >> 2)), c, x.A) : 0.f;
-        }
-        *reinterpret_cast<f32x4*>(raw + pc * 1024 + lane * 16) = e;
-    }
-    return 0;
-}
-
-// s_waitcnt vmcnt(n) for a runtime n (the loader's DMAs just issued stay in flight).
-__device__ __forceinline__ void hxsWaitVm(int n) {
-#define GAR_VM(v) case v: __builtin_amdgcn_s_waitcnt(((v) & 15) | (((v) >> 4) << 14) | 0x0F70); break;
-    switch (n) {
-        GAR_VM(0) GAR_VM(1) GAR_VM(2) GAR_VM(3) GAR_VM(4) GAR_VM(5) GAR_VM(6) GAR_VM(7) GAR_VM(8) GAR_VM(9)
-        GAR_VM(10) GAR_VM(11) GAR_VM(12) GAR_VM(13) GAR_VM(14) GAR_VM(15) GAR_VM(16) GAR_VM(17) GAR_VM(18)
-        GAR_VM(19) GAR_VM(20) GAR_VM(21) GAR_VM(22) GAR_VM(23) GAR_VM(24) GAR_VM(25) GAR_VM(26) GAR_VM(27)
-        GAR_VM(28) GAR_VM(29) GAR_VM(30) GAR_VM(31) GAR_VM(32)
-        default: __builtin_amdgcn_s_waitcnt(0x0F70); break;
-    }
-#undef GAR_VM
+template <class XP>
+__device__ __forceinline__ HxsStage hxsLoad(XP x, int b, int j, int P) {
+    const int GQ = x->G * x->Qc;
+    if (j < P) return hxsStage(x, b, j * GQ, min(GQ, x->Wg - j * GQ));
+    return hxsStage(x, b, x->Wg + (j - P) * GQ, GQ);
 }
 
 // One item (row `row` of the stage, quad q) -> ring rows (hi/lo split, mirror, loud marking).
-__device__ __forceinline__ void hxsPutItem(const HxsArgs& x, const HxsStage& st, int p0, int q, int row, f32x4 e,
+template <class XP>
+__device__ __forceinline__ void hxsPutItem(XP x, const HxsStage& st, int p0, int q, int row, f32x4 e,
                                            char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
     const int t = st.T0 + row;  // column-relative row
     int p = p0 + row;           // ring row (nrow <= R)
-    if (p >= x.R) p -= x.R;
+    if (p >= x->R) p -= x->R;
     const bool l0 = hxLoud(e[0]), l1 = hxLoud(e[1]), l2 = hxLoud(e[2]), l3 = hxLoud(e[3]);
     if (__builtin_expect(l0 | l1 | l2 | l3, 0)) {
         if (l0) { atomicMin(loudLo + 4 * q, t); atomicMax(loudHi + 4 * q, t); e[0] = 0.f; }
@@ -368,141 +277,101 @@ __device__ __forceinline__ void hxsPutItem(const HxsArgs& x, const HxsStage& st,
     hxSplit2(e[2], e[3], hv.y, lv.y);
     char* qb = ring + q * QS;
     *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
-    *reinterpret_cast<uint2*>(qb + 8 * x.Rt + 8 * p) = lv;
-    if (p < x.mirror) {
-        p += x.R;
+    *reinterpret_cast<uint2*>(qb + 8 * x->Rt + 8 * p) = lv;
+    if (p < x->mirror) {
+        p += x->R;
         *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
-        *reinterpret_cast<uint2*>(qb + 8 * x.Rt + 8 * p) = lv;
-    }
-}
-
-// Every wave: its share of a staged raw buffer -> ring.  Items are (quad, row)
-// with rows padded to 64 so a wave instruction covers 64 consecutive rows of
-// one quad (conflict-free raw reads and ring writes); thread t of nth takes
-// items t, t + nth, ...
-__device__ __forceinline__ void hxsConvert(const HxsArgs& x, const HxsStage& st, const char* raw, int tid, int nth,
-                                           char* ring, uint32_t QS, int* loudLo, int* loudHi, int* flag) {
-    const int pad = (st.nrow + 63) & ~63;
-    const int p0 = uni(st.T0 % x.R);  // ring row of the stage's first row
-    // two items per pass: their raw reads are in flight together
-    for (int j0 = 0; j0 < kHxsConvMax; j0 += 2) {
-        if (j0 * nth >= 4 * pad) break;  // uniform
-        f32x4 e[2];
-        int q[2], row[2];
-        bool ok[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int i = tid + (j0 + u) * nth;
-            q[u] = (i >= pad) + (i >= 2 * pad) + (i >= 3 * pad);
-            row[u] = i - q[u] * pad;
-            ok[u] = q[u] <= 3 && row[u] < st.nrow;
-            const int qq = ok[u] ? q[u] : 0, rr = ok[u] ? row[u] : 0;
-            if (x.fmt == 1) {
-                const char* sp = raw + (rr >> 7) * 8192 + (rr & 127) * 8 + (2 * qq) * 1024;
-                const f2v a = *reinterpret_cast<const f2v*>(sp);
-                const f2v c = *reinterpret_cast<const f2v*>(sp + 1024);
-                e[u] = f32x4{a.x, a.y, c.x, c.y};
-            } else {
-                e[u] = *reinterpret_cast<const f32x4*>(raw + (rr >> 4) * 1024 + (rr & 15) * 64 + qq * 16);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (ok[u]) hxsPutItem(x, st, p0, q[u], row[u], e[u], ring, QS, loudLo, loudHi, flag);
+        *reinterpret_cast<uint2*>(qb + 8 * x->Rt + 8 * p) = lv;
     }
 }
 
 // Small launches (x.small: one macro period per column, one group): every wave gathers
 // its share of the block's whole window [0, Wg) straight into the ring in one pass --
 // one memory round trip instead of the pipeline's chain of DMA stages.
-__device__ __forceinline__ void hxsSmallStage(const HxsArgs& x, int b, int tid, int nth, char* ring, uint32_t QS,
+template <class XP>
+__device__ __forceinline__ void hxsSmallStage(XP x, int b, int tid, int nth, char* ring, uint32_t QS,
                                               int* loudLo, int* loudHi, int* flag) {
     const HxsArgsP xc = hxsCold();
     const SrcDesc src = kload(&xc->src);
     HxsStage st;
     st.T0 = 0;
-    st.nrow = x.Wg;
+    st.nrow = x->Wg;
     st.fast = false;
-    for (int i = tid; i < 4 * x.Wg; i += nth) {
+    for (int i = tid; i < 4 * x->Wg; i += nth) {
         const int q = i & 3, row = i >> 2;
         f32x4 e;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const int col = b * 16 + 4 * q + n;
-            const int k = col / x.C, c = col - k * x.C;
-            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, row), c, x.A) : 0.f;
+            const int k = col / x->C, c = col - k * x->C;
+            e[n] = col < x->ncols ? hxsGather(src, hxsChunkRow(x, k, row), c, x->A) : 0.f;
         }
         hxsPutItem(x, st, 0, q, row, e, ring, QS, loudLo, loudHi, flag);
     }
 }
 
-// ---- register staging (x.regs) ----------------------------------------------------
-// Loader wave q owns quad q (columns 4q..4q+3) of the block.  A load (rows
-// [T0, T0 + nrow) of the four columns) is kHxsNP pieces of 64 rows, lane l
-// holding row T0 + 64i + l of piece i as one f32x4 (the quad's four columns):
-//   STEREO  (fmt 1): chunks 2q, 2q+1, both channels -> two buffer_load_dwordx2
-//   ROW16   (fmt 2): channels 4q..4q+3 of one chunk  -> one buffer_load_dwordx4
-//   general (fmt 0): each column its own resource      -> four buffer_load_dword
-// Loads are issued kHxsD steps before their conversion (the compiler tracks
-// them: vmcnt waits only for the oldest), so about 3 x (G*Qc rows x 16 columns
-// x 4 B) per CU are in flight against HBM latency, and the raw data never
-// touches LDS.  Rows past the caller's input read zeros through the records.
-// Registers of one load, per format: STEREO two f2v per piece (chunks 2q, 2q+1), ROW16 one f32x4.
-// One loop per format (hxsRegLoadersT<FMT>), so a loaded register is never merged with another
-// format's value (a merge would be a copy, and a copy waits for the load).
+// ---- register staging -------------------------------------------------------------
+// One load's registers per loader wave: STEREO two f2v per item, ROW16 one f32x4.  One loop per
+// format (hxsRegLoadersT<FMT>), so a loaded register is never merged with another format's
+// value (a merge is a copy, and a copy waits for the load).
 template <int FMT>
 struct HxsRegBuf {
-    f2v a[kHxsNP], b[kHxsNP];
+    f2v a[kHxsItems], b[kHxsItems];
 };
 template <>
 struct HxsRegBuf<2> {
-    f32x4 v[kHxsNP];
+    f32x4 v[kHxsItems];
+};
+template <>
+struct HxsRegBuf<3> {  // STEREO PCM16: one dword (both channels) per chunk row
+    uint32_t a[kHxsItems], b[kHxsItems];
 };
 
-// Per-block load resources of loader wave q (fmt 1: chunks 2q, 2q+1; fmt 2: the block's chunk at
-// channel offset c0) and its lane's byte offset from row 0.
+// Per-block load source: one resource from the block's first chunk row 0 (records end at the
+// caller's input end: zeros past it), the byte stride of a row and of a chunk.
 struct HxsRegSrc {
-    __amdgpu_buffer_rsrc_t a, b;
-    int lane0, pieceB, rowB;  // lane's offset of row 0, bytes per 64-row piece, bytes per row
+    __amdgpu_buffer_rsrc_t r;
+    int rowB, chunkB, lane0;
 };
 
-template <int FMT>
-__device__ __forceinline__ HxsRegSrc hxsRegSrc(const HxsArgs& x, int b, int q, int lane) {
+template <int FMT, class XP>
+__device__ __forceinline__ HxsRegSrc hxsRegSrc(XP x, int b, int lane) {
     HxsRegSrc r;
-    if (FMT == 1) {
-        const int k0 = (b * 16) >> 1;
-        r.a = hxsRsrcT(x, hxsChunkRow(x, k0 + 2 * q, 0), 0, 8);
-        r.b = hxsRsrcT(x, hxsChunkRow(x, k0 + 2 * q + 1, 0), 0, 8);
-        r.rowB = 8;
-        r.lane0 = lane * 8;
-    } else {
-        const int col0 = b * 16, k = col0 / x.C, c0 = col0 - k * x.C;
-        r.rowB = static_cast<int>(x.in_fs) * 4;
-        r.a = hxsRsrcT(x, hxsChunkRow(x, k, 0), c0, 64);
-        r.b = r.a;
-        r.lane0 = lane * r.rowB + 16 * q;
-    }
-    r.pieceB = 64 * r.rowB;
+    const int col0 = b * 16, k = col0 / x->C, c0 = col0 - k * x->C;
+    r.rowB = static_cast<int>(x->in_fs) * x->in_esz;
+    r.chunkB = x->Np * x->Qc * r.rowB;
+    r.r = hxsRsrcT(x, hxsChunkRow(x, k, 0), FMT == 2 ? c0 : 0, FMT == 2 ? 64 : (FMT == 3 ? 4 : 8));
+    r.lane0 = lane * r.rowB;
     return r;
 }
 
-// Always kHxsNP pieces (x2 for STEREO) of load instructions, whatever the load: pieces it does not
-// need (past its rows, or a whole edge/absent load, `live` false) get an offset past every record,
-// which returns zeros without a memory access.  A fixed instruction pattern lets the compiler's
-// vmcnt tracking wait for exactly the oldest load; a conditional issue would make it wait for all.
+// Issue load `st` (live: a real load; else nothing to fetch).  Always the same instruction
+// pattern, kHxsItems x (2 STEREO | 1 ROW16) loads: items the load does not need (past its
+// rows, dead loads, edge loads that are gathered later) get an offset past every record,
+// which returns zeros without a memory access -- the compiler's vmcnt tracking then waits
+// for exactly the oldest load (a conditional issue would make it wait for all).
 template <int FMT>
-__device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, HxsRegBuf<FMT>& r) {
+__device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxsRegBuf<FMT>& r) {
     const bool fast = FMT != 0 && live && st.fast;
     const int npc = fast ? (st.nrow + 63) >> 6 : 0;
-    const int voff = st.T0 * rs.rowB + rs.lane0;
+    const int base = st.T0 * rs.rowB + rs.lane0;
 #pragma unroll
-    for (int i = 0; i < kHxsNP; ++i) {
-        const int o = i < npc ? voff + rs.pieceB * i : static_cast<int>(0x80000000u);
+    for (int k = 0; k < kHxsItems; ++k) {
+        const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
+        const bool on = it < 4 * kHxsNP && i < npc;
         if constexpr (FMT == 2) {
-            r.v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.a, o, 0, 0));
-        } else if constexpr (FMT == 1) {
-            r.a[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.a, o, 0, 0));
-            r.b[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.b, o, 0, 0));
+            const int o = on ? base + 64 * i * rs.rowB + 16 * q : static_cast<int>(0x80000000u);
+            r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
+        } else if constexpr (FMT == 1 || FMT == 4) {  // f32 / int32 stereo frames
+            const int o = on ? base + 64 * i * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + rs.chunkB : o;
+            r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
+            r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
+        } else if constexpr (FMT == 3) {  // int16 stereo frames
+            const int o = on ? base + 64 * i * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + rs.chunkB : o;
+            r.a[k] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, o, 0, 0);
+            r.b[k] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, o2, 0, 0);
         }
     }
     return fast;
@@ -536,17 +405,17 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
 }
 
 // The per-block protocol shared by both roles (identical barrier sequences).
-// Loads j = 0 .. P + ngroups - 2 (hxsLoad) go through raw buffer j % 3:
-//   reset B | loaders issue loads 0, 1, wait load 0 B |
-//   step j = 0 .. P + ngroups - 1: every wave converts load j; loaders issue
-//   load j + 2 and wait load j + 1; compute waves run MFMA group j - P (when
-//   >= 0: stage 0 and stages 1 .. j - P are in the ring); B | [fixup]
-// Steps of a block (P stage-0 parts + ngroups groups), padded to a multiple of kHxsD under
-// register staging so the loaders' unrolled loop issues the same loads on every path.
+// Loads j = 0 .. P + ngroups - 2 (hxsLoad: the P parts of stage 0, then stages 1 ..):
+//   reset B | loaders issue loads 0 .. kHxsD-1 | B |
+//   step j = 0 .. stepsPad - 1: loaders convert load j (registers -> ring) and issue load
+//   j + kHxsD; compute waves run MFMA group j - P (when 0 <= j - P < ngroups: stage 0 and
+//   stages 1 .. j - P are in the ring); B | [fixup]
+// Steps of a block (P stage-0 parts + ngroups groups), padded to a multiple of kHxsD so the
+// loaders' unrolled loop issues the same loads on every path.
 __device__ __forceinline__ int hxsStepsPad(const HxsArgs& x) {
     const int GQ = x.G * x.Qc;
     const int n = (x.small ? 0 : (x.Wg + GQ - 1) / GQ) + x.ngroups;
-    return kHxsRegs ? (n + kHxsD - 1) / kHxsD * kHxsD : n;
+    return (n + kHxsD - 1) / kHxsD * kHxsD;
 }
 
 struct HxsShared {
@@ -555,38 +424,57 @@ struct HxsShared {
     int* loudLo;
     int* loudHi;
     int* flag;
-    char* raw;  // [3][stageBytes]
 };
 
-// Register staging: load `st` -> ring rows of quad q, from the registers of its
-// issue (fast) or gathered now (edge stages: history seam, partial blocks).
-template <int FMT>
-__device__ __forceinline__ void hxsRegConvert(const HxsArgs& x, const HxsStage& st, bool fast, const HxsRegBuf<FMT>& r,
-                                              int b, int q, int lane, const HxsShared& sh) {
-    const int p0 = uni(st.T0 % x.R);
-    const int npc = (st.nrow + 63) >> 6;
-    if (FMT != 0 && fast) {
+// Register staging: loader l's items of load `st` -> ring rows, from the registers of its issue
+// (fast) or gathered now (edge loads).
+template <int FMT, class XP>
+__device__ __forceinline__ void hxsRegConvert(XP x, const HxsStage& st, bool fast, const HxsRegBuf<FMT>& r,
+                                              int b, int l, int lane, const HxsShared& sh) {
+    const int p0 = uni(st.T0 % x->R);
+    if (FMT != 0 && fast) {  // straight-line: registers -> ring
 #pragma unroll
-        for (int i = 0; i < kHxsNP; ++i) {
-            const int row = 64 * i + lane;
-            if (i < npc && row < st.nrow) {
+        for (int k = 0; k < kHxsItems; ++k) {
+            const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
+            if (it < 4 * kHxsNP && 64 * i < st.nrow) {  // uniform
                 f32x4 e;
-                if constexpr (FMT == 2) e = r.v[i];
-                else e = f32x4{r.a[i].x, r.a[i].y, r.b[i].x, r.b[i].y};
-                hxsPutItem(x, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+                if constexpr (FMT == 2) {
+                    e = r.v[k];
+                } else if constexpr (FMT == 1) {
+                    e = f32x4{r.a[k].x, r.a[k].y, r.b[k].x, r.b[k].y};
+                } else if constexpr (FMT == 3) {  // int16 pairs -> float64(i) * (1 / 32767) -> f32
+                    const uint32_t ua = r.a[k], ub = r.b[k];
+                    e = f32x4{static_cast<float>(pcmToF64(static_cast<int16_t>(ua & 0xffffu), 16)),
+                              static_cast<float>(pcmToF64(static_cast<int16_t>(ua >> 16), 16)),
+                              static_cast<float>(pcmToF64(static_cast<int16_t>(ub & 0xffffu), 16)),
+                              static_cast<float>(pcmToF64(static_cast<int16_t>(ub >> 16), 16))};
+                } else {  // FMT 4: int32 pairs (PCM24 / PCM32)
+                    const int bits = x->in_pcm;
+                    e = f32x4{static_cast<float>(pcmToF64(__builtin_bit_cast(int32_t, r.a[k].x), bits)),
+                              static_cast<float>(pcmToF64(__builtin_bit_cast(int32_t, r.a[k].y), bits)),
+                              static_cast<float>(pcmToF64(__builtin_bit_cast(int32_t, r.b[k].x), bits)),
+                              static_cast<float>(pcmToF64(__builtin_bit_cast(int32_t, r.b[k].y), bits))};
+                }
+                const int row = 64 * i + lane;
+                if (row < st.nrow) hxsPutItem(x, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
             }
         }
         return;
     }
     const HxsArgsP xc = hxsCold();
     const SrcDesc src = kload(&xc->src);
-    for (int row = lane; row < st.nrow; row += 64) {
+#pragma unroll 1
+    for (int k = 0; k < kHxsItems; ++k) {
+        const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
+        const int row = 64 * i + lane;
+        if (it >= 4 * kHxsNP || 64 * i >= st.nrow) break;  // uniform (items ascend in i)
+        if (row >= st.nrow) continue;
         f32x4 e;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
             const int col = b * 16 + 4 * q + n;
-            const int k = col / x.C, c = col - k * x.C;
-            e[n] = col < x.ncols ? hxsGather(src, hxsChunkRow(x, k, st.T0 + row), c, x.A) : 0.f;
+            const int kk = col / x->C, c = col - kk * x->C;
+            e[n] = col < x->ncols ? hxsGather(src, hxsChunkRow(x, kk, st.T0 + row), c, x->A) : 0.f;
         }
         hxsPutItem(x, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
     }
@@ -620,7 +508,7 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
         hxsBarrier();  // loud state reset; the previous block's ring reads done
-        if (x.small) hxsSmallStage(x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        if (x.small) hxsSmallStage(&x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
         hxsBarrier();  // load 0 landed (small: the whole window in the ring)
         const int col = b * 16 + l16;
         const bool colOk = col < x.ncols;
@@ -634,7 +522,7 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             const int64_t o0 = a * x.Pc + oRow0;
             const bool live = colOk && p < x.Np && a < x.a_hi;
             if (x.dbg & 2) {
-            } else if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+            } else if (fullRb && live && !x.out_pcm && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
                 char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
                 hxsStoreFast<VST>(x, pp, y, lane);
             } else if (live) {
@@ -643,7 +531,8 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
                     const int64_t o = o0 + i;
                     if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi) {
                         char* pp = x.out + o * x.out_fs + ccol * x.out_cs;
-                        if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
+                        if (x.out_pcm) pcmWrite(pp, 0, x.out_pcm, static_cast<double>(y[i]));
+                        else if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
                         else *reinterpret_cast<float*>(pp) = y[i];
                     }
                 }
@@ -653,9 +542,6 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
         for (int j = 0; j < nstepsPad; ++j) {
             // load j -> ring (this wave's share), then the MFMA periods of group j - P
             const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            if (!kHxsRegs && j < nL && !((x.dbg & 16) && j >= P) && !((x.dbg & 32) && j >= P))
-                hxsConvert(x, hxsLoad(x, b, j, P), sh_.raw + (j % 3) * x.stageBytes, tid, nth, sh_.ring, QS,
-                           sh_.loudLo, sh_.loudHi, sh_.flag);
             if (x.prof) tcv += __builtin_amdgcn_s_memtime() - t0;
             const int g = j - P;
             if (g < 0 || g >= x.ngroups) {
@@ -732,45 +618,53 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     }
 }
 
-// Register-staging loader wave q (x.regs): same barrier sequence as the compute
+// Loader wave l: same barrier sequence as the compute
 // waves; in step j it converts load j (issued kHxsD steps earlier) into the ring
 // and issues load j + kHxsD into the registers just freed.
 template <int FMT>
-__device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared& sh_, int q, int lane) {
-    const int GQ = x.G * x.Qc;
-    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
+__device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared& sh_, int l, int lane) {
+    // Every argument is read through an opaque kernarg pointer renewed per step (hxsCold), so
+    // the scalar loads sit next to their uses instead of pinning ~70 SGPRs for the whole
+    // kernel (spilled SGPRs cost a v_readlane per use inside the conversion).
+    HxsArgsP xp = hxsCold();
+    const int GQ = xp->G * xp->Qc;
+    const int P = xp->small ? 0 : (xp->Wg + GQ - 1) / GQ, nL = xp->small ? 0 : P + xp->ngroups - 1;
     const int nstepsPad = hxsStepsPad(x);
-    const int tid = (x.nprog + q) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
-    unsigned long long pc = 0, pi = 0, pb = 0;
-    const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+    const int tid = (x.nprog + l) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    for (int bi = blockIdx.x; bi < xp->nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
-        if (q == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
-        if (q == 0 && lane == 0) *sh_.flag = 0;
+        if (l == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
+        if (l == 0 && lane == 0) *sh_.flag = 0;
         hxsBarrier();  // loud state reset; the previous block's ring reads done
         HxsRegBuf<FMT> buf[kHxsD];
         bool fastL[kHxsD];
-        const HxsRegSrc rs = hxsRegSrc<FMT>(x, b, q, lane);
+        const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
 #pragma unroll
-        for (int d = 0; d < kHxsD; ++d) fastL[d] = hxsRegIssue<FMT>(hxsLoad(x, b, d, P), d < nL, rs, buf[d]);
-        if (x.small) hxsSmallStage(x, b, tid, nth, sh_.ring, sh_.QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        for (int d = 0; d < kHxsD; ++d) fastL[d] = hxsRegIssue<FMT>(hxsLoad(xp, b, d, P), d < nL, rs, l, buf[d]);
+        if (xp->small) hxsSmallStage(xp, b, tid, nth, sh_.ring, sh_.QS, sh_.loudLo, sh_.loudHi, sh_.flag);
         hxsBarrier();  // (small: the whole window in the ring)
         for (int j0 = 0; j0 < nstepsPad; j0 += kHxsD) {
 #pragma unroll
             for (int d = 0; d < kHxsD; ++d) {
                 const int j = j0 + d;
-                const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-                if (j < nL && !((x.dbg & 16) && j >= P))
-                    hxsRegConvert<FMT>(x, hxsLoad(x, b, j, P), fastL[d], buf[d], b, q, lane, sh_);
-                const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-                fastL[d] = hxsRegIssue<FMT>(hxsLoad(x, b, j + kHxsD, P), j + kHxsD < nL && !((x.dbg & 1) && j >= P), rs,
-                                            buf[d]);
-                const unsigned long long t2 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-                hxsBarrier();  // step done: load j in the ring
-                if (x.prof) {
-                    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-                    pc += t1 - t0; pi += t2 - t1; pb += t3 - t2;
+                xp = hxsCold();
+                const int dbg = xp->dbg;
+                if ((dbg & 64) && j >= P) {  // development: consume the registers, no conversion
+                    float s = 0.f;
+#pragma unroll
+                    for (int k = 0; k < kHxsItems; ++k) {
+                        if constexpr (FMT == 2) s += buf[d].v[k][0] + buf[d].v[k][3];
+                        else if constexpr (FMT == 1 || FMT == 4) s += buf[d].a[k].x + buf[d].b[k].y;
+                        else if constexpr (FMT == 3) s += static_cast<float>(buf[d].a[k] ^ buf[d].b[k]);
+                    }
+                    if (s == 1234.5f) sh_.loudLo[0] = 0;
+                } else if (j < nL && !((dbg & 16) && j >= P)) {
+                    hxsRegConvert<FMT>(xp, hxsLoad(xp, b, j, P), fastL[d], buf[d], b, l, lane, sh_);
                 }
+                if (!(dbg & 128))  // development: no issue at all (the skeleton's cost without dummy loads)
+                    fastL[d] = hxsRegIssue<FMT>(hxsLoad(xp, b, j + kHxsD, P), j + kHxsD < nL && !((dbg & 1) && j >= P), rs,
+                                                l, buf[d]);
+                hxsBarrier();  // step done: load j in the ring
             }
         }
         if (*sh_.flag) {
@@ -779,94 +673,14 @@ __device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared
             hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
         }
     }
-    if (x.prof && lane == 0) {
-        atomicAdd(x.prof + 0, pc);
-        atomicAdd(x.prof + 1, pi);
-        atomicAdd(x.prof + 2, pb);
-        atomicAdd(x.prof + 3, 1ull);
-        atomicAdd(x.prof + 9, __builtin_amdgcn_s_memrealtime() - rStart);
-    }
 }
 
-__device__ __forceinline__ void hxsRegLoaders(const HxsArgs& x, const HxsShared& sh_, int q, int lane) {
-    if (x.fmt == 1) hxsRegLoadersT<1>(x, sh_, q, lane);
-    else if (x.fmt == 2) hxsRegLoadersT<2>(x, sh_, q, lane);
-    else hxsRegLoadersT<0>(x, sh_, q, lane);
-}
-
-// Loader waves: the DMAs (or gathers) of every stage, two groups ahead, and their share of the conversion.
-__device__ __forceinline__ void hxsLoaders(const HxsArgs& x, const HxsShared& sh_, int wl, int lane) {
-    if (kHxsRegs) {
-        hxsRegLoaders(x, sh_, wl, lane);
-        return;
-    }
-    const int GQ = x.G * x.Qc;
-    const int tid = (x.nprog + wl) * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
-    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
-    unsigned long long tc = 0, tl = 0, tb = 0, ti = 0, tpre = 0, tloop = 0;
-    const unsigned long long rStart = x.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
-        const int b = hxsBlock(x, bi);
-        if (wl == 0 && lane < 16) { sh_.loudLo[lane] = INT_MAX; sh_.loudHi[lane] = -1; }
-        if (wl == 0 && lane == 0) *sh_.flag = 0;
-        hxsBarrier();  // loud state reset; the previous block's ring reads done
-        if (x.small) {
-            hxsSmallStage(x, b, tid, nth, sh_.ring, sh_.QS, sh_.loudLo, sh_.loudHi, sh_.flag);
-        } else {
-            hxsIssue(x, hxsLoad(x, b, 0, P), b, wl, lane, sh_.raw);
-            hxsWaitVm(nL > 1 ? hxsIssue(x, hxsLoad(x, b, 1, P), b, wl, lane, sh_.raw + x.stageBytes) : 0);
-        }
-        hxsBarrier();  // load 0 landed (small: the whole window in the ring)
-        if (x.prof) tpre += __builtin_amdgcn_s_memrealtime() - rStart;
-        for (int j = 0; j < P + x.ngroups; ++j) {
-            const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            const bool solo = (x.dbg & 32) && j >= P;  // loaders convert the whole load
-            if (j < nL && !((x.dbg & 16) && j >= P))
-                hxsConvert(x, hxsLoad(x, b, j, P), sh_.raw + (j % 3) * x.stageBytes, solo ? wl * 64 + lane : tid,
-                           solo ? 64 * kHxsLoaders : nth, sh_.ring, sh_.QS,
-                           sh_.loudLo, sh_.loudHi, sh_.flag);
-            const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            const int nd = (j + 2 < nL && !((x.dbg & 1) && j >= P))
-                               ? hxsIssue(x, hxsLoad(x, b, j + 2, P), b, wl, lane, sh_.raw + ((j + 2) % 3) * x.stageBytes)
-                               : 0;
-            const unsigned long long t1b = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            hxsWaitVm(nd);  // load j + 1 landed
-            const unsigned long long t2 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            if (x.prof) ti += t1b - t1;
-            hxsBarrier();  // step done
-            if (x.prof) {
-                const unsigned long long t3 = __builtin_amdgcn_s_memtime();
-                tc += t1 - t0; tl += t2 - t1; tb += t3 - t2;
-            }
-        }
-        if (x.prof) tloop = __builtin_amdgcn_s_memrealtime();
-        if (*sh_.flag) {
-            __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
-            hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
-        }
-    }
-    if (x.prof && lane == 0) {
-        const unsigned long long rEnd = __builtin_amdgcn_s_memrealtime();
-        atomicAdd(x.prof + 8, tpre);
-        atomicAdd(x.prof + 12, rEnd - tloop);
-        atomicAdd(x.prof + 0, tc);
-        atomicAdd(x.prof + 1, tl);
-        atomicAdd(x.prof + 2, tb);
-        atomicAdd(x.prof + 3, 1ull);
-        atomicAdd(x.prof + 7, ti);
-        atomicAdd(x.prof + 9, rEnd - rStart);
-        if (wl == 0 && blockIdx.x < 4096) {  // per-workgroup start / life of the last launch
-            x.prof[64 + 2 * blockIdx.x] = rStart;
-            x.prof[65 + 2 * blockIdx.x] = rEnd - rStart;
-        }
-        if (x.nblocks > 16) {
-            atomicMin(x.prof + 10, rStart);
-            atomicMax(x.prof + 11, rEnd);
-            atomicMin(x.prof + 13, rEnd - rStart);
-            atomicMax(x.prof + 14, rEnd - rStart);
-        }
-    }
+__device__ __forceinline__ void hxsRegLoaders(const HxsArgs& x, const HxsShared& sh_, int l, int lane) {
+    if (x.fmt == 1) hxsRegLoadersT<1>(x, sh_, l, lane);
+    else if (x.fmt == 2) hxsRegLoadersT<2>(x, sh_, l, lane);
+    else if (x.fmt == 3) hxsRegLoadersT<3>(x, sh_, l, lane);
+    else if (x.fmt == 4) hxsRegLoadersT<4>(x, sh_, l, lane);
+    else hxsRegLoadersT<0>(x, sh_, l, lane);
 }
 
 template <int NS, int VST>
@@ -878,11 +692,10 @@ __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
     s.loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(s.QS));
     s.loudHi = s.loudLo + 16;
     s.flag = s.loudHi + 16;
-    s.raw = reinterpret_cast<char*>(smem + 4 * static_cast<size_t>(s.QS) + 256);
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
     if (wt < x.nprog) hxsCompute<NS, VST>(x, s, wt, lane);
-    else hxsLoaders(x, s, wt - x.nprog, lane);
+    else hxsRegLoaders(x, s, wt - x.nprog, lane);
 }
 
 // Launch (explicitly instantiated in gar_hxs_i*.hip).

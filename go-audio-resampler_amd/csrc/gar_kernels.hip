@@ -90,7 +90,7 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     g.nblocks = (g.ncols + tileN - 1) / tileN;
     g.dbg = knobDbg;
     g.vst = 0;
-    if (!p.f64 && !od.f64 && !knobNoVst) {
+    if (!p.f64 && !od.f64 && !od.pcm && !knobNoVst) {
         if (od.fs == 1) g.vst = 1;
         else if (C == 2 && od.fs == 2 && od.cs == 1) g.vst = 2;
     }
@@ -268,6 +268,32 @@ hipError_t launchCopy(const void* src, int src_f64, int64_t s_fs, int64_t s_cs, 
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(copy_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, src, src_f64, s_fs, s_cs,
                        dst, dst_f64, d_fs, d_cs, n, C);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void convert_kernel(const void* s, int st, int64_t sfs, int64_t scs, void* d, int dt,
+                                                      int64_t dfs, int64_t dcs, int64_t n, int C) {
+    const int64_t total = n * C;
+    for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; idx < total;
+         idx += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t t = idx / C;
+        const int c = static_cast<int>(idx - t * C);
+        const int64_t se = t * sfs + c * scs, de = t * dfs + c * dcs;
+        const double v = st >= 16 ? pcmRead(s, se, st)
+                                  : (st == 1 ? static_cast<const double*>(s)[se] : static_cast<double>(static_cast<const float*>(s)[se]));
+        if (dt >= 16) pcmWrite(d, de, dt, v);
+        else if (dt == 1) static_cast<double*>(d)[de] = v;
+        else static_cast<float*>(d)[de] = static_cast<float>(v);
+    }
+}
+
+hipError_t launchConvert(const void* src, int s_type, int64_t s_fs, int64_t s_cs, void* dst, int d_type, int64_t d_fs,
+                         int64_t d_cs, int64_t n, int C, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    int64_t blocks = (n * C + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(convert_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, src, s_type, s_fs, s_cs,
+                       dst, d_type, d_fs, d_cs, n, C);
     return hipGetLastError();
 }
 

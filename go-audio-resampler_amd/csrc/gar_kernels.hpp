@@ -18,6 +18,7 @@ struct SrcDesc {
     const void* in;
     int64_t in_base, in_len, in_fs, in_cs;
     int in_f64;
+    int in_pcm;            // 0 float input, else PCM bits (16: int16, 24/32: int32 storage)
     int64_t valid_end;
 };
 
@@ -26,8 +27,26 @@ struct OutDesc {
     void* out;
     int64_t o0, fs, cs;
     int f64;
+    int pcm;               // 0 float output, else PCM bits (int(clamp(y, -1, 1) * maxVal))
     int64_t o_lo, o_hi;
 };
+
+// Integer PCM <-> float, after cmd/resample-wav/main.go:444-543 (maxInt16/24/32, main.go:54-56):
+// in = float64(i) * (1 / maxVal); out = int(clamp(float64(y), -1, 1) * maxVal), truncating.
+__host__ __device__ inline double pcmMax(int bits) {
+    return bits == 16 ? 32767.0 : (bits == 24 ? 8388607.0 : 2147483647.0);
+}
+__host__ __device__ inline int pcmBytes(int bits) { return bits == 16 ? 2 : 4; }
+__host__ __device__ inline double pcmToF64(int32_t i, int bits) { return static_cast<double>(i) * (1.0 / pcmMax(bits)); }
+__host__ __device__ inline double pcmRead(const void* p, int64_t e, int bits) {
+    return bits == 16 ? pcmToF64(static_cast<const int16_t*>(p)[e], 16) : pcmToF64(static_cast<const int32_t*>(p)[e], bits);
+}
+__host__ __device__ inline void pcmWrite(void* p, int64_t e, int bits, double y) {
+    const double v = y > 1.0 ? 1.0 : (y < -1.0 ? -1.0 : y);  // NaN passes through as in Go, then converts
+    const double s = v * pcmMax(bits);
+    if (bits == 16) static_cast<int16_t*>(p)[e] = static_cast<int16_t>(s == s ? static_cast<int32_t>(s) : 0);
+    else static_cast<int32_t*>(p)[e] = s == s ? static_cast<int32_t>(s) : 0;
+}
 
 struct HxDev;
 
@@ -98,5 +117,8 @@ hipError_t launchGather(int f64, const SrcDesc& src, void* dst, int64_t t0, int6
 // Strided copy with dtype conversion (pass-through stages, group split).
 hipError_t launchCopy(const void* src, int src_f64, int64_t s_fs, int64_t s_cs, void* dst, int dst_f64,
                       int64_t d_fs, int64_t d_cs, int64_t n, int C, hipStream_t stream);
+// PCM staging of the non-fused paths: type codes 0 f32, 1 f64, 16/24/32 PCM (pcmRead / pcmWrite).
+hipError_t launchConvert(const void* src, int s_type, int64_t s_fs, int64_t s_cs, void* dst, int d_type, int64_t d_fs,
+                         int64_t d_cs, int64_t n, int C, hipStream_t stream);
 
 }  // namespace gar

@@ -298,8 +298,11 @@ class Resampler:
         return lib().gar_channels(self._h)
 
     # -- device-resident (torch tensors on cuda) --
-    def process_device(self, x, out=None, stream=None):
-        """x: [frames, channels] device tensor (float32/float64, any strides).  Returns out[:n].
+    def process_device(self, x, out=None, stream=None, pcm_bits=None):
+        """x: [frames, channels] device tensor (float32/float64, or integer PCM: int16 = PCM16,
+        int32 = PCM24/PCM32 per pcm_bits, default 32), any strides.  Returns out[:n] (out
+        allocated with x's dtype if None).  Integer PCM follows cmd/resample-wav/main.go:444-543
+        (input i * (1/maxVal), output int(clamp(y, -1, 1) * maxVal)).
         x.shape[1] (and out.shape[1]) must equal Channels (ErrChannelMismatch)."""
         import torch
         assert x.is_cuda and x.dim() == 2
@@ -313,15 +316,15 @@ class Resampler:
         if out is None:
             out = torch.empty((max(n, 1), x.shape[1]), dtype=x.dtype, device=x.device)
         got = C.c_int64(0)
-        dt = F64 if x.dtype == torch.float64 else F32
-        odt = F64 if out.dtype == torch.float64 else F32
+        dt = _io_type(x.dtype, pcm_bits)
+        odt = _io_type(out.dtype, pcm_bits)
         st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream)
         _check(lib().gar_process_device(self._h, C.c_void_p(x.data_ptr()), dt, x.stride(0), x.stride(1), frames,
                                         x.shape[1], C.c_void_p(out.data_ptr()), odt, out.stride(0), out.stride(1),
                                         out.shape[0], C.byref(got), st))
         return out[: got.value]
 
-    def flush_device(self, out=None, dtype=None, stream=None):
+    def flush_device(self, out=None, dtype=None, stream=None, pcm_bits=None):
         import torch
         if out is not None and out.shape[1] != self.Channels:
             raise ErrChannelMismatch(f"expected {self.Channels} channels, got {out.shape[1]}")
@@ -331,11 +334,31 @@ class Resampler:
         if out is None:
             out = torch.empty((max(n, 1), self.Channels), dtype=dtype or torch.float32, device="cuda")
         got = C.c_int64(0)
-        odt = F64 if out.dtype == torch.float64 else F32
+        odt = _io_type(out.dtype, pcm_bits)
         st = C.c_void_p(stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream)
         _check(lib().gar_flush_device(self._h, out.shape[1], C.c_void_p(out.data_ptr()), odt, out.stride(0),
                                       out.stride(1), out.shape[0], C.byref(got), st))
         return out[: got.value]
+
+
+PCM16, PCM24, PCM32 = 16, 24, 32
+
+
+def _io_type(dtype, pcm_bits=None):
+    """Device sample type code of a torch dtype (gar.h GAR_F32/GAR_F64/GAR_PCM*)."""
+    import torch
+    if dtype == torch.float64:
+        return F64
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.int16:
+        return PCM16
+    if dtype == torch.int32:
+        bits = pcm_bits or PCM32
+        if bits not in (PCM24, PCM32):
+            raise ValueError("int32 PCM holds 24- or 32-bit samples")
+        return bits
+    raise TypeError(f"unsupported sample dtype {dtype}")
 
 
 def New(config):

@@ -48,6 +48,13 @@ enum { GAR_FLAG_NO_INTERPOLATION = 1, GAR_FLAG_MINIMUM_PHASE = 2, GAR_FLAG_LINEA
  * f16-split products on the f16 matrix cores, f32 accumulation, error <= exact-f32 arithmetic's),
  * GAR_F32_EXACT (exact f32 products on the f32 matrix cores). */
 enum { GAR_F64 = 0, GAR_F32 = 1, GAR_F32_EXACT = 2 };
+/* integer PCM sample types of the device entry points (in_dtype / out_dtype of gar_process_device
+ * and gar_flush_device), after cmd/resample-wav/main.go:444-543: input sample i -> float64(i) *
+ * (1 / maxVal) in the compute type; output y -> int(clamp(float64(y), -1, 1) * maxVal) (truncation),
+ * maxVal = 32767 (PCM16, int16 storage), 8388607 (PCM24, int32 storage), 2147483647 (PCM32, int32).
+ * Fused into the split-f16 kernel's loads and stores for single-stage float32 plans; staged
+ * through a conversion kernel otherwise. */
+enum { GAR_PCM16 = 16, GAR_PCM24 = 24, GAR_PCM32 = 32 };
 /* engine.Quality (internal/engine/filter_params.go:16-41), for gar_design_engine */
 enum { GAR_ENGINE_QUICK = 0, GAR_ENGINE_LOW, GAR_ENGINE_MEDIUM, GAR_ENGINE_HIGH, GAR_ENGINE_VERYHIGH,
        GAR_ENGINE_16BIT, GAR_ENGINE_20BIT, GAR_ENGINE_24BIT, GAR_ENGINE_28BIT, GAR_ENGINE_32BIT };
