@@ -47,7 +47,7 @@ PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
 PEAK_F64_MATRIX_TFLOPS = 78.6
 # reference-algorithm flops per input sample
 REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6, "poly": None,
-                  "quick": None}
+                  "quick": None, "pcm16": 1017.6}
 DECIM_MACS_PER_INPUT = 611.5  # cfg5 stage 1: factor 2, 1223 taps
 # New path: preset -> precision -> engine quality (stages.go:54-70, pipeline_builder.go:76-100)
 ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit, "Quick": lambda g: g.EngineQuick}
@@ -76,6 +76,10 @@ WORKLOADS = {
                  io="f32", compute="F32", streams=1, scaling="weak", chunk=0, kind_bytes={4: 4 * (4 + 2.75625)},
                  desc="stereo float32 16k->44.1k QualityHigh: DFT x2 stage, then DFT x2 + polyphase with a "
                       "fractional step (x != 0, poly_kernel), 600 s, one Process+Flush"),
+    "pcm16": dict(name="pcm16_stereo_int16_44k1_48k_q24_600s", ir=44100, orr=48000, ch=2, preset="High", seconds=600.0,
+                  io="pcm16", compute="F32", streams=1, scaling="weak", chunk=0,
+                  desc="cfg2 geometry on 16-bit integer PCM I/O (resample-wav main.go:444-543 scaling/clamp fused "
+                       "into the kernel's loads and stores), 600 s, one Process+Flush"),
     "quick": dict(name="quick_stereo_f32_44k1_48k_600s", ir=44100, orr=48000, ch=2, preset="Quick", seconds=600.0,
                   io="f32", compute="F32", streams=1, scaling="weak", chunk=0, kind_bytes={5: 4 * (1 + 48000 / 44100)},
                   desc="stereo float32 44.1k->48k QualityQuick (CubicStage), 600 s, one Process+Flush"),
@@ -85,7 +89,7 @@ WORKLOADS = {
 def metric_for(key, w):
     if key == "cfg2":
         return BASELINE_METRIC
-    io = "float32" if w["io"] == "f32" else "float64"
+    io = {"f32": "float32", "f64": "float64", "pcm16": "int16 PCM"}[w["io"]]
     return (f"Msamples/s resampled ({io}, {w['ir'] / 1000:g}k→{w['orr'] / 1000:g}k Quality{w['preset']}, "
             f"{w['ch'] * w['streams']} ch) + RMS error vs Go ref")
 
@@ -307,11 +311,16 @@ def main():
         s_lo, s_hi = rank, rank + 1  # one stream (batch) per rank
     n_streams = s_hi - s_lo
     C = w["ch"] * (n_streams if w["scaling"] == "strong" else 1)
-    tdt = torch.float32 if w["io"] == "f32" else torch.float64
+    tdt = {"f32": torch.float32, "f64": torch.float64, "pcm16": torch.int16}[w["io"]]
+    pcm_scale = 1.0 / 32767.0 if w["io"] == "pcm16" else None  # main.go:54, :449-460
     x_host = None
     if args.workload == "cfg2":  # the exact generator of the round-1 line (numpy, per-channel seeds)
         x_host = synth_stream(frames, C, 4242 + 2 * s_lo, w["ir"])
         x = torch.from_numpy(x_host).to(dev)
+    elif pcm_scale:
+        xs = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], torch.float32)
+        x = torch.round(xs.clamp(-1, 1) * (32767 * 0.98)).to(torch.int16)
+        del xs
     else:
         x = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], tdt)
 
@@ -338,9 +347,14 @@ def main():
         tail = r.flush_device(out=yf)
         return o, tail.shape[0]
 
+    inline_prof = os.environ.get("GAR_BENCH_PROF_INLINE", "1") == "1"
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if inline_prof:  # HIP events around every launch inside the timed region (on the launch stream)
+        r.profile(True)
+        for k in range(6):
+            r.profile_read(k)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -351,15 +365,13 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    # kernel durations for the roofline: the same K steps again with the library's HIP events
-    # around every launch (on the launch stream) -- a separate pass, so the event packets do not
-    # stretch the timed steps above
-    r.profile(True)
-    for k in range(6):
-        r.profile_read(k)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
+    if not inline_prof:  # development: a separate profiled pass (the timed steps carry no event packets)
+        r.profile(True)
+        for k in range(6):
+            r.profile_read(k)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
     prof = {k: r.profile_read(k) for k in range(6)}
     r.profile(False)
 
@@ -376,10 +388,16 @@ def main():
         preset = getattr(O, "P_" + w["preset"].upper())
         m = min(frames, int(args.check_seconds * w["ir"]))
         got = y[:n_proc].double().cpu().numpy()
+        if pcm_scale:  # PCM: both sides in full-scale units (the oracle is fed the kernel's f32 inputs)
+            got = got * pcm_scale
+
+        def xin(a):
+            a = np.asarray(a, dtype=np.float64)
+            return (a * pcm_scale).astype(np.float32).astype(np.float64) if pcm_scale else a
         chans = sorted({0, C - 1})
         errs = []
         for c in chans:
-            xc = (x_host[:m, c] if x_host is not None else x[:m, c].cpu().numpy()).astype(np.float64)
+            xc = xin(x_host[:m, c] if x_host is not None else x[:m, c].cpu().numpy())
             ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
             want = ref.process(xc, 0)
             errs.append(np.mean((got[: len(want), c] - want) ** 2))
@@ -393,10 +411,10 @@ def main():
             k = max(0, (frames - m) // Qc)
             m0 = k * Qc
             skip = 4 * geom.fir_taps_max
-            tail = yf[:n_tail].double().cpu().numpy()
+            tail = yf[:n_tail].double().cpu().numpy() * (pcm_scale or 1.0)
             errs = []
             for c in chans:
-                xc = (x_host[m0:, c] if x_host is not None else x[m0:, c].cpu().numpy()).astype(np.float64)
+                xc = xin(x_host[m0:, c] if x_host is not None else x[m0:, c].cpu().numpy())
                 ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
                 want = np.concatenate([ref.process(xc, 0), ref.flush(0)])
                 full = np.concatenate([got[k * Pc:, c], tail[:, c]])
@@ -412,7 +430,7 @@ def main():
     dom = max((0, 1, 2, 4, 5), key=lambda k: prof[k][0])
     kms, launches = prof[dom]
     launch_s = (kms / 1e3) / max(launches, 1)
-    in_bytes = 4 if w["io"] == "f32" else 8
+    in_bytes = {"f32": 4, "f64": 8, "pcm16": 2}[w["io"]]
     out_samples_step = (n_proc + n_tail) * C
     if w["compute"] == "F32" and dom in w.get("kind_bytes", {}):
         # that stage's own stream bytes per input frame and channel (its input read once, output written once)
@@ -468,7 +486,7 @@ def main():
     # streaming drop-in usage (rank 0): 4096-frame (cfg5: 4800) chunks through the device
     # API and through the host C-ABI (ProcessMulti over planar float64, the cgo shim's call)
     streaming = None
-    if rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak":
+    if rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak" and w["io"] == "f32":
         streaming = time_streaming(gar, torch, w, x, C, dev)
 
     line = {
@@ -498,8 +516,11 @@ def main():
                             else f"independent streams, 1 per GPU x {world}"),
         },
         "roofline": roof,
-        "arith": ("f32 I/O; products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
-                  "(error at the level of exact-f32 arithmetic: rms_vs_oracle)" if w["compute"] == "F32"
+        "arith": (("int16 PCM I/O converted in the kernel's loads (float64(i)/32767 -> f32) and stores "
+                   "(clamp, x32767, truncate); rms_vs_oracle in full-scale units includes the output "
+                   "quantization (~0.6 LSB = 1.8e-5); " if pcm_scale else "f32 I/O; ") +
+                  "products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
+                  "(error at the level of exact-f32 arithmetic)" if w["compute"] == "F32"
                   else "f64 I/O and f64 MFMA (v_mfma_f64_16x16x4_f64)"),
         "streaming": streaming,
         "cpu_baseline": None,

@@ -459,9 +459,8 @@ hipError_t timed(Ctx& x, int tag, L&& launch) {
         b = x.h->evPool.back().second;
         x.h->evPool.pop_back();
     } else {
-        // timing only: no system-scope fence (it would add an L2 writeback to the timed launch)
-        HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
-        HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
     }
     HIPCHK(hipEventRecord(a, x.s));
     const hipError_t e = launch();

@@ -120,7 +120,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const int64_t ncols = nchunk * C;
     if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorNotSupported;
 
-    // group size: largest G <= 3 (LDS, DMAs per loader, staged items per thread) not above Np
+    // group size: largest G <= kHxsMaxG that fits the LDS ring and the loaders' registers, not above Np
     auto ringFor = [&](int G, int& R, int& Rt, int& Wg) {
         const int GQ = G * static_cast<int>(Qc);
         Wg = (G - 1) * static_cast<int>(Qc) + p.Kread;
@@ -150,7 +150,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         return hxsLds(Rt) <= 160 * 1024 && (GQ + 63) / 64 <= kHxsNP;
     };
     int G = 0, R = 0, Rt = 0, Wg = 0;
-    for (int cand = small ? 1 : 3; cand >= 1; --cand) {
+    for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
         int r, rt, wg;
         ringFor(cand, r, rt, wg);
         if (cand > 1 && cand > Np) continue;
@@ -201,7 +201,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.out_fs = od.fs * esz;
     x.out_cs = od.cs * esz;
     const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
-    if (od.pcm) x.vst = 0;  // PCM stores: the epilogue's checked per-element path
+    if (od.pcm == 16 && al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;  // int16 stereo frame pairs
+    else if (od.pcm) x.vst = 0;  // other PCM stores: the epilogue's checked per-element path
     else if (od.f64) x.vst = 3;
     else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;
     else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;

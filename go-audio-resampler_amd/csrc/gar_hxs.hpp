@@ -35,10 +35,14 @@ namespace gar {
 constexpr int kHxsLoaders = GAR_HXS_L;                  // loader waves per workgroup
 constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 waves per SIMD, 128 VGPRs)
 #ifndef GAR_HXS_D
-#define GAR_HXS_D 3
+#define GAR_HXS_D 2
 #endif
 constexpr int kHxsD = GAR_HXS_D;                        // loads in flight per loader wave (register staging)
-constexpr int kHxsNP = 7;                               // 64-row pieces per load (G*Qc <= 448)
+#ifndef GAR_HXS_NP
+#define GAR_HXS_NP 10
+#endif
+constexpr int kHxsNP = GAR_HXS_NP;                      // 64-row pieces per load (G*Qc <= 640: cfg2 G = 4)
+constexpr int kHxsMaxG = 6;                             // periods per group (launcher: largest that fits)
 constexpr int kHxsItems = (4 * kHxsNP + kHxsLoaders - 1) / kHxsLoaders;  // (quad, piece) items per loader per load
 
 struct HxsArgs {
@@ -377,6 +381,13 @@ __device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const
     return fast;
 }
 
+// int(clamp(float64(y), -1, 1) * 32767) with pcmWrite's semantics (f64 product: exact; NaN -> 0).
+__device__ __forceinline__ int32_t pcm16Of(float y) {
+    const double d = static_cast<double>(y);
+    const double v = (d > 1.0 ? 1.0 : (d < -1.0 ? -1.0 : d)) * 32767.0;
+    return v == v ? static_cast<int32_t>(v) : 0;
+}
+
 template <int VST>
 __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y, int lane) {
     if (VST == 2) {
@@ -387,8 +398,17 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
         f32x4 w;
         if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
         else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
-        if (x.nt) __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
-        else *reinterpret_cast<f32x4*>(p) = w;
+        if (x.out_pcm == 16) {  // two int16 stereo frames (8 B): clamp, x32767, truncate (main.go:497-541)
+            const int32_t i0 = pcm16Of(w[0]), i1 = pcm16Of(w[1]), i2 = pcm16Of(w[2]), i3 = pcm16Of(w[3]);
+            uint2 v;
+            v.x = (static_cast<uint32_t>(i0) & 0xffffu) | (static_cast<uint32_t>(i1) << 16);
+            v.y = (static_cast<uint32_t>(i2) & 0xffffu) | (static_cast<uint32_t>(i3) << 16);
+            *reinterpret_cast<uint2*>(p) = v;
+        } else if (x.nt) {
+            __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
+        } else {
+            *reinterpret_cast<f32x4*>(p) = w;
+        }
     } else if (VST == 1) {
         if (x.nt) __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(p));
         else *reinterpret_cast<f32x4*>(p) = y;
@@ -522,7 +542,7 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             const int64_t o0 = a * x.Pc + oRow0;
             const bool live = colOk && p < x.Np && a < x.a_hi;
             if (x.dbg & 2) {
-            } else if (fullRb && live && !x.out_pcm && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+            } else if (fullRb && live && (!x.out_pcm || VST == 2) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
                 char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
                 hxsStoreFast<VST>(x, pp, y, lane);
             } else if (live) {

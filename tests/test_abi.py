@@ -227,3 +227,32 @@ def test_get_info_fields(gar, O, i, o, preset):
             s0.poly_taps_per_phase * s0.poly_phases
         assert (inf.FilterLength, inf.Phases) == (want, s0.poly_phases)
     assert inf.MemoryUsage > 0
+
+
+def test_device_api_sample_types(gar):
+    """The device entry points accept float32/float64 and integer PCM (GAR_PCM16/24/32,
+    resample-wav main.go:444-543) and refuse any other sample type before touching memory;
+    a dry handle runs the PCM calls through the stream-length state machine."""
+    import ctypes as C
+    r = gar.New(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True))
+    got = C.c_int64(0)
+    for bad in (3, 8, 17, 64, -1):
+        rc = gar.lib().gar_process_device(r._h, None, bad, 2, 1, 0, 2, None, gar.F32, 2, 1, 1000, C.byref(got), None)
+        assert rc == gar.INVALID_ARGUMENT, bad
+        rc = gar.lib().gar_flush_device(r._h, 2, None, bad, 2, 1, 1000, C.byref(got), None)
+        assert rc == gar.INVALID_ARGUMENT, bad
+    n = gar.lib().gar_device_output_size(r._h, 4410)
+    for t in (gar.PCM16, gar.PCM24, gar.PCM32):
+        r.Reset()
+        rc = gar.lib().gar_process_device(r._h, C.c_void_p(1), t, 2, 1, 4410, 2, C.c_void_p(1), t, 2, 1, n, C.byref(got), None)
+        assert rc == gar.GAR_OK and got.value == n
+    assert gar._io_type.__doc__
+
+
+def test_pcm_constants_match_header(gar):
+    """gar.h GAR_PCM16/24/32 equal the Python mirror's codes (the bit depth)."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "gar.h")).read()
+    m = re.search(r"GAR_PCM16 = (\d+), GAR_PCM24 = (\d+), GAR_PCM32 = (\d+)", hdr)
+    assert m and tuple(int(v) for v in m.groups()) == (gar.PCM16, gar.PCM24, gar.PCM32)
