@@ -469,8 +469,9 @@ hipError_t timed(Ctx& x, int tag, L&& launch) {
     return e;
 }
 
-hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C) {
-    return timed(x, tag, [&] { return launchBg(p, src, od, C, x.s); });
+hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C,
+                   HistCopy* hc = nullptr) {
+    return timed(x, tag, [&] { return launchBg(p, src, od, C, x.s, hc); });
 }
 
 SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
@@ -608,10 +609,25 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             bool quirk = false;
             const int64_t nout = cntPoly(c, d.poly, nu, quirk);
             if (!c.staged) {
-                // Fused: DFT x2 and polyphase composed into one MFMA FIR over x.
-                if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C));
+                // Fused: DFT x2 and polyphase composed into one MFMA FIR over x; the history keep
+                // x[u_base/2, x_count) rides along in the same launch when the kernel takes it.
+                HistCopy hc;
+                const int64_t k0 = c.u_base / 2, k1 = std::max(k0, c.x_count);
+                Hist& hs = dv.xh;
+                if (x.launch && nout > 0 && !quirk && !rt.f64 && k1 > k0) {
+                    hs.buf[1 - hs.cur].ensure(static_cast<size_t>(k1 - k0) * C * 4);
+                    hc.dst = hs.buf[1 - hs.cur].p;
+                    hc.t0 = k0;
+                    hc.n = k1 - k0;
+                }
+                if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C, &hc));
                 if (quirk) {
                     materialize(x, rt, c, dv, xsrc);
+                } else if (hc.done) {
+                    hs.cur = 1 - hs.cur;
+                    hs.base = k0;
+                    hs.len = k1 - k0;
+                    hs.zero = false;
                 } else {
                     hist_update(x, dv.xh, xsrc, c.u_base / 2, c.x_count);
                 }

@@ -36,12 +36,12 @@ int64_t ceilDiv(int64_t a, int64_t b) { return -floorDiv(-a, b); }
 
 }  // namespace
 
-hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
+hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // row-block plans stream through the wave-specialised kernel (GAR_HXS=0: the block kernel, A/B runs)
     static const bool hxs = !(std::getenv("GAR_HXS") && std::getenv("GAR_HXS")[0] == '0');
     if (p.rb && hxs) {
-        const hipError_t e = launchHxs(p, src, od, C, stream);
+        const hipError_t e = launchHxs(p, src, od, C, stream, hc);
         if (e != hipErrorNotSupported) return e;
     }
     if (od.pcm) return hipErrorNotSupported;  // PCM output is fused into hxs_kernel only (engine stages it otherwise)

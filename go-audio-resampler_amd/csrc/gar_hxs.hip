@@ -83,7 +83,7 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256; }
 
 // hipErrorNotSupported: the plan does not fit this kernel's geometry (the caller uses hx_kernel).
-hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
+hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return hipErrorNotSupported;
     static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
@@ -224,6 +224,12 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
                 x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
                 (long long)x.fastLo, (long long)x.fastHi);
+    if (hc && hc->n > 0 && hc->dst) {  // history keep folded into this launch (no gather_kernel after it)
+        x.hdst = static_cast<float*>(hc->dst);
+        x.ht0 = hc->t0;
+        x.hn = hc->n;
+        hc->done = true;
+    }
     const size_t lds = hxsLds(Rt);
     const int64_t blocks = x.nblocks;
     switch (p.NS) {

@@ -65,6 +65,8 @@ struct HxsArgs {
     int64_t in_fs, in_cs, fastLo, fastHi;
     int in_esz, in_pcm;    // bytes per input element; PCM bits (0: float input)
     int out_pcm;           // PCM output bits (0: float output; stores go through the checked path)
+    float* hdst;           // folded history keep (HistCopy): hdst[(t - ht0) * C + c] = src(t, c), t < ht0 + hn
+    int64_t ht0, hn;
     char* out;             // output (o, c) at out + o*out_fs + c*out_cs (bytes), o absolute
     int64_t out_fs, out_cs;
     int out_f64;
@@ -716,6 +718,16 @@ __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
     const int wt = uni(threadIdx.x >> 6);
     if (wt < x.nprog) hxsCompute<NS, VST>(x, s, wt, lane);
     else hxsRegLoaders(x, s, wt - x.nprog, lane);
+    if (x.hn > 0) {  // history keep for the next call (launchGather's job, folded into this launch)
+        const HxsArgsP xc = hxsCold();
+        const SrcDesc src = kload(&xc->src);
+        const int64_t total = x.hn * x.C;
+        for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+             i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+            const int64_t t = i / x.C;
+            x.hdst[i] = srcRead<float>(src, x.ht0 + t, static_cast<int>(i - t * x.C));
+        }
+    }
 }
 
 // Launch (explicitly instantiated in gar_hxs_i*.hip).

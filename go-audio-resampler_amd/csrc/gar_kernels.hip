@@ -40,10 +40,10 @@ hipError_t bgLaunchF32a(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                         size_t lds, int64_t blocks, hipStream_t st, bool globalB);
 
-hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream) {
+hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // f32 compute on the split-f16 kernel (every output of the launch, any input dtype)
-    if (p.hx && !p.f64) return launchHx(*p.hx, src, od, C, stream);
+    if (p.hx && !p.f64) return launchHx(*p.hx, src, od, C, stream, hc);
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;

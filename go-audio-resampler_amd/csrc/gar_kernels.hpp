@@ -102,10 +102,22 @@ struct CubicSeg {
 constexpr int64_t kCubicSegInputs = 256;
 
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
-hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
-hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+// Optional history keep folded into a streaming FIR launch: dst[(t - t0) * C + c] = src(t, c) for
+// t in [t0, t0 + n) (what launchGather does), written by the launch's workgroups after their
+// blocks; `done` set when the launch took it (hxs_kernel only), else the caller gathers.
+struct HistCopy {
+    void* dst = nullptr;
+    int64_t t0 = 0, n = 0;
+    bool done = false;
+};
+
+hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
+                    HistCopy* hc = nullptr);
+hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
+                    HistCopy* hc = nullptr);
 // Streaming wave-specialised variant of launchHx for row-block plans (gar_hxs.hip).
-hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream);
+hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
+                     HistCopy* hc = nullptr);
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, int64_t nout, int C,
                       hipStream_t stream);
 // CubicStage outputs of nseg checkpointed segments (segs readable by the device:

@@ -335,16 +335,26 @@ static uint16_t f16bits(double v) {
 
 bool buildHxPlan(const FirPeriodic& f, HxPlan& plan) {
     if (f.P <= 0 || f.Q <= 0) return false;
-    int bestMp = 1;
-    double bestEff = -1;
+    // macro period: the best MFMA efficiency among the ones whose row blocks fit the streaming
+    // kernel (one compute wave per row block, <= kHxRbMaxNS steps: hxs_kernel, gar_hxs.hpp), else
+    // the best overall (segmented programs on hx_kernel)
+    int bestMp = 1, bestRbMp = 0;
+    double bestEff = -1, bestRbEff = -1;
     for (int mp = 1; mp <= 64; ++mp) {
         const int Pc = f.P * mp;
         if (Pc > 320) break;
         double eff;
-        geomFor(f, mp, eff, kHxStep, 1);
+        const std::vector<RbGeom> g = geomFor(f, mp, eff, kHxStep, 1);
         if (Pc < 16) eff *= static_cast<double>(Pc) / 16.0;
         if (eff > bestEff + 1e-9) { bestEff = eff; bestMp = mp; }
+        int ml = 0;
+        for (const auto& r : g) ml = std::max(ml, r.nsteps);
+        if (static_cast<int>(g.size()) <= kHxRbMaxWaves && ml <= kHxRbMaxNS && eff > bestRbEff + 1e-9) {
+            bestRbEff = eff;
+            bestRbMp = mp;
+        }
     }
+    if (bestRbMp > 0) bestMp = bestRbMp;
     double eff;
     const std::vector<RbGeom> rbs = geomFor(f, bestMp, eff, kHxStep, 1);
     plan = HxPlan();
