@@ -39,9 +39,9 @@ constexpr int kHxsWaves = kHxRbMaxWaves + kHxsLoaders;  // __launch_bounds__ (4 
 #endif
 constexpr int kHxsD = GAR_HXS_D;                        // loads in flight per loader wave (register staging)
 #ifndef GAR_HXS_NP
-#define GAR_HXS_NP 10
+#define GAR_HXS_NP 12
 #endif
-constexpr int kHxsNP = GAR_HXS_NP;                      // 64-row pieces per load (G*Qc <= 640: cfg2 G = 4)
+constexpr int kHxsNP = GAR_HXS_NP;                      // 64-row pieces per load (G*Qc <= 768: cfg2 G = 5)
 constexpr int kHxsMaxG = 6;                             // periods per group (launcher: largest that fits)
 constexpr int kHxsItems = (4 * kHxsNP + kHxsLoaders - 1) / kHxsLoaders;  // (quad, piece) items per loader per load
 
