@@ -55,6 +55,8 @@ struct BgGrid {
     int C, nprog, kch, nwt, ncg, nred, nslots, parity;
     int dbg;  // development timing knob (GAR_BG_DBG): 1 skip tile DMA after the first, 2 skip stores
     int vst;  // f32 epilogue: 0 scalar, 1 channel-contiguous (fs == 1), 2 stereo interleaved (C == 2, fs == 2, cs == 1)
+    void* hdst;       // folded history keep (HistCopy): hdst[(t - ht0) * C + c] = src(t, c), t < ht0 + hn
+    int64_t ht0, hn;
 };
 
 // f32 epilogue of one 16x16 accumulator: lane holds rows r0..r0+3 (r0 =
@@ -419,6 +421,14 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                 // its barrier orders this reduction before the buffer's reuse
                 if (!g.parity) __syncthreads();
             }
+        }
+    }
+    if (g.hn > 0) {  // history keep for the next call (launchGather's job, folded into this launch)
+        const int64_t total = g.hn * g.C;
+        for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+             i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+            const int64_t t = i / g.C;
+            static_cast<TC*>(g.hdst)[i] = srcRead<TC>(src, g.ht0 + t, static_cast<int>(i - t * g.C));
         }
     }
 }

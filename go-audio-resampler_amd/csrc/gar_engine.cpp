@@ -518,6 +518,29 @@ void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
     hs.zero = false;
 }
 
+// A FIR launch `l(HistCopy*)` (when `launch`) with the history keep hs <- src[k0, k1) folded into it
+// when the kernel takes it (hxs_kernel, bg_kernel); otherwise the keep is a gather launch after it.
+template <class L>
+void withHist(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1, bool launch, L&& l) {
+    HistCopy hc;
+    const int other = 1 - hs.cur;
+    if (x.launch && launch && k1 > k0) {
+        hs.buf[other].ensure(static_cast<size_t>(k1 - k0) * x.g->C * (x.h->f64 ? 8 : 4));
+        hc.dst = hs.buf[other].p;
+        hc.t0 = k0;
+        hc.n = k1 - k0;
+    }
+    if (x.launch && launch) HIPCHK(l(&hc));
+    if (hc.done) {
+        hs.cur = other;
+        hs.base = k0;
+        hs.len = k1 - k0;
+        hs.zero = false;
+    } else {
+        hist_update(x, hs, src, k0, k1);
+    }
+}
+
 // FUSED -> STAGED: rebuild the poly-stream history u[u_base, u_count) from x by
 // the DFT plan and keep the DFT's own history x[x_count - dft_hist, x_count).
 void materialize(Ctx& x, StageRT& rt, Counters& c, StageDev& dv, const SrcDesc& xsrc) {
@@ -585,8 +608,8 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t y0 = c.y_count;
             const int64_t nout = cntDft(c, d.dft, n);
             const SrcDesc src = mkSrc(dv.xh, C, x0, in);
-            if (x.launch && nout > 0) HIPCHK(timedBg(x, 1, rt.dftD, src, mkOut(out, y0, nout), C));
-            hist_update(x, dv.xh, src, c.x_count - c.dft_hist, c.x_count);
+            withHist(x, dv.xh, src, c.x_count - c.dft_hist, c.x_count, nout > 0,
+                     [&](HistCopy* hc) { return timedBg(x, 1, rt.dftD, src, mkOut(out, y0, nout), C, hc); });
             c.y_count += nout;
             return nout;
         }
@@ -595,8 +618,8 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             const int64_t y0 = c.y_count;
             const int64_t nout = cntDecim(c, d.decim, n);
             const SrcDesc src = mkSrc(dv.xh, C, x0, in);
-            if (x.launch && nout > 0) HIPCHK(timedBg(x, 2, rt.decimD, src, mkOut(out, y0, nout), C));
-            hist_update(x, dv.xh, src, c.x_count - c.dec_hist, c.x_count);
+            withHist(x, dv.xh, src, c.x_count - c.dec_hist, c.x_count, nout > 0,
+                     [&](HistCopy* hc) { return timedBg(x, 2, rt.decimD, src, mkOut(out, y0, nout), C, hc); });
             c.y_count += nout;
             return nout;
         }
@@ -611,38 +634,25 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             if (!c.staged) {
                 // Fused: DFT x2 and polyphase composed into one MFMA FIR over x; the history keep
                 // x[u_base/2, x_count) rides along in the same launch when the kernel takes it.
-                HistCopy hc;
-                const int64_t k0 = c.u_base / 2, k1 = std::max(k0, c.x_count);
-                Hist& hs = dv.xh;
-                if (x.launch && nout > 0 && !quirk && !rt.f64 && k1 > k0) {
-                    hs.buf[1 - hs.cur].ensure(static_cast<size_t>(k1 - k0) * C * 4);
-                    hc.dst = hs.buf[1 - hs.cur].p;
-                    hc.t0 = k0;
-                    hc.n = k1 - k0;
-                }
-                if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C, &hc));
                 if (quirk) {
+                    if (x.launch && nout > 0) HIPCHK(timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C));
                     materialize(x, rt, c, dv, xsrc);
-                } else if (hc.done) {
-                    hs.cur = 1 - hs.cur;
-                    hs.base = k0;
-                    hs.len = k1 - k0;
-                    hs.zero = false;
                 } else {
-                    hist_update(x, dv.xh, xsrc, c.u_base / 2, c.x_count);
+                    withHist(x, dv.xh, xsrc, c.u_base / 2, c.x_count, nout > 0, [&](HistCopy* hc) {
+                        return timedBg(x, 0, rt.fusedD, xsrc, mkOut(out, y0, nout), C, hc);
+                    });
                 }
             } else {
                 // Staged: DFT (MFMA FIR) into u scratch, polyphase with live cubic interpolation.
                 const int64_t p0 = before.x_count - before.dft_hist;   // DFT positions done before
                 const int64_t dy0 = p0 * d.dft.factor;
                 InView uin;
-                if (x.launch) {
-                    x.g->utmp.ensure(static_cast<size_t>(std::max<int64_t>(nu, 1)) * C * rt.tc());
-                    if (nu > 0) {
-                        OutView uv{x.g->utmp.p, C, 1, rt.f64 ? 1 : 0};
-                        HIPCHK(timedBg(x, 1, rt.dftD, xsrc, mkOut(uv, dy0, nu), C));
-                    }
-                }
+                if (x.launch) x.g->utmp.ensure(static_cast<size_t>(std::max<int64_t>(nu, 1)) * C * rt.tc());
+                // the x history keep depends on x only: it rides in the DFT launch
+                withHist(x, dv.xh, xsrc, c.x_count - c.dft_hist, c.x_count, nu > 0, [&](HistCopy* hc) {
+                    OutView uv{x.g->utmp.p, C, 1, rt.f64 ? 1 : 0};
+                    return timedBg(x, 1, rt.dftD, xsrc, mkOut(uv, dy0, nu), C, hc);
+                });
                 uin.p = x.g->utmp.p; uin.fs = C; uin.cs = 1; uin.f64 = rt.f64 ? 1 : 0; uin.n = nu;
                 const SrcDesc usrc = mkSrc(dv.uh, C, before.u_count, uin);
                 if (x.launch && nout > 0) {
@@ -651,7 +661,6 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                     p.u_base = before.u_base;
                     HIPCHK(timed(x, 4, [&] { return launchPoly(p, usrc, mkOut(out, y0, nout), nout, C, x.s); }));
                 }
-                hist_update(x, dv.xh, xsrc, c.x_count - c.dft_hist, c.x_count);
                 if (nu > 0) hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
             }
             c.y_count += nout;

@@ -102,6 +102,14 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t blocks = std::min<int64_t>(g.nblocks, static_cast<int64_t>(ncu) * (knobWgPerCu > 0 ? knobWgPerCu : 2));
+    g.hdst = nullptr;
+    g.ht0 = g.hn = 0;
+    if (hc && hc->n > 0 && hc->dst) {  // history keep folded into this launch (no gather_kernel after it)
+        g.hdst = hc->dst;
+        g.ht0 = hc->t0;
+        g.hn = hc->n;
+        hc->done = true;
+    }
     if (p.f64) return bgLaunchF64(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
     if (p.NS < 56) return bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
     return bgLaunchF32b(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
