@@ -9,8 +9,10 @@
 //    LDS with ds_read_b64_tr_b16, runs the MFMAs and stores its outputs.  They
 //    issue no global loads, so no s_waitcnt on vector memory ever stalls an
 //    MFMA stream (on gfx950 stores and loads share vmcnt).  The last
-//    kHxsLoaders waves are loader waves: they stream the input rows into LDS,
-//    convert them to the f16 hi/lo split and detect loud elements.
+//    kHxsLoaders waves are loader waves: they load the input rows into VGPRs
+//    kHxsD groups ahead (a fixed buffer-load pattern the compiler's vmcnt
+//    tracking pipelines), convert them to the f16 hi/lo split (or from integer
+//    PCM first), detect loud elements and write the LDS ring.
 //  * Long columns.  A column is (channel, chunk of Np consecutive macro
 //    periods); a workgroup owns 16 columns and walks them group by group (G
 //    periods per group, one barrier per group).  Each column's window lives
