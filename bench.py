@@ -48,7 +48,6 @@ PEAK_F64_MATRIX_TFLOPS = 78.6
 # reference-algorithm flops per input sample
 REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6, "poly": None,
                   "quick": None, "pcm16": 1017.6}
-DECIM_MACS_PER_INPUT = 611.5  # cfg5 stage 1: factor 2, 1223 taps
 # New path: preset -> precision -> engine quality (stages.go:54-70, pipeline_builder.go:76-100)
 ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit, "Quick": lambda g: g.EngineQuick}
 
@@ -222,7 +221,7 @@ def cpu_baseline(w, target_s=10.0):
             "cpu_model": model, "nproc": ncpu, "cpus_usable": avail}
 
 
-def pmc_traffic(args, kernel_keys):
+def pmc_traffic(args, workload, kernel_keys):
     """HBM bytes per launch of the dominant kernel, measured now: two rocprofv3 PMC
     passes (FETCH_SIZE, then WRITE_SIZE: 3 + 2 TCC counters do not fit one pass)
     over a short child run of this same workload; corrected as
@@ -241,8 +240,9 @@ def pmc_traffic(args, kernel_keys):
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="gar_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.join(ROOT, "bench.py"), "--workload", args.workload, "--steps", "2",
-               "--warmup", "1", "--no-cpu-baseline", "--check-seconds", "0", "--no-pmc", "--no-streaming"]
+               sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload, "--steps", "2",
+               "--warmup", "1", "--no-cpu-baseline", "--check-seconds", "0", "--no-pmc", "--no-streaming",
+               "--secondary", "none"]
         try:
             p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                  start_new_session=True)
@@ -271,39 +271,45 @@ def pmc_traffic(args, kernel_keys):
         gmax = max(grid.values())
         vals = [v for k, v in per.items() if grid[k] == gmax]
         out[counter] = sum(vals) / len(vals)
-    rd = out["FETCH_SIZE"] * 1024 * 2
+    corr = FETCH_CORRECTION[LOAD_WIDTH.get(workload, 16)]
+    rd = out["FETCH_SIZE"] * 1024 * corr
     wr = out["WRITE_SIZE"] * 1024
-    return {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr}, None
+    return {"read_bytes": rd, "write_bytes": wr, "bytes": rd + wr, "fetch_correction": corr}, None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--seconds", type=float, default=None, help="stream length override")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the live PMC traffic passes")
-    ap.add_argument("--no-streaming", action="store_true", help="skip the chunked drop-in timing")
-    ap.add_argument("--check-seconds", type=float, default=5.0, help="prefix (and suffix) checked against the oracle")
-    args = ap.parse_args()
-    w = dict(WORKLOADS[args.workload])
-    if args.seconds:
-        w["seconds"] = args.seconds
+# bytes per lane of the dominant kernel's streaming input loads (gar_hxs.hpp hxsRegIssue: STEREO
+# buffer_load_dwordx2, ROW16 dwordx4, PCM16 stereo dword; f64 bg_kernel LDS-DMA dwordx4)
+LOAD_WIDTH = {"cfg2": 8, "cfg4": 8, "ns256": 16, "cfg3": 16, "pcm16": 4, "cfg5": 16, "poly": 4, "quick": 4}
+KIND_NAMES = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)",
+              4: "polyphase with live cubic coefficients (poly_kernel)", 5: "QualityQuick cubic stage (cubic_kernel)"}
+# profile kind -> engine kind of the stage it runs (gar_engine_geometry.kind: 1 DFT-only, 2 DFT+poly, 3 decim, 0 cubic)
+KIND_STAGE = {0: (2,), 1: (1, 2), 2: (3,), 4: (2,), 5: (0,)}
+# gfx950 FETCH_SIZE under-count per load width (MI355X_MICROARCH.md HBM section: x2 for 16-B/lane
+# streaming reads; other widths calibrated on a known byte count, profiles/r03_fetch_calib.txt)
+FETCH_CORRECTION = {16: 2.0, 8: 2.0, 4: 2.0}
 
-    import torch
+
+def secondary_default(primary, world):
+    """Workloads timed beside the primary line (each with its own ms, roofline and PMC traffic):
+    the north-star 256-ch stream, BASELINE configs[2], configs[4] and -- the scaling config,
+    at every world size -- configs[3]."""
+    if primary != "cfg2":
+        return []
+    return ["ns256", "cfg3", "cfg5", "cfg4"] if world == 1 else ["cfg4"]
+
+
+def run_workload(key, args, steps, warmup, world, rank, dev, primary):
+    """Time `steps` steps (after `warmup`) of workload `key` on this rank; returns its JSON
+    object (value = all ranks' input samples / max-over-ranks wall time) and the dominant
+    kernel's rocprof name keys."""
     import gar
-
-    world, rank, local = dist_env()
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
+    w = dict(WORKLOADS[key])
+    if primary and args.seconds:
+        w["seconds"] = args.seconds
+    dry = args.dry_run
+    torch = None
+    if not dry:
+        import torch
     frames = int(round(w["seconds"] * w["ir"]))
     if w["scaling"] == "strong":
         s_lo, s_hi = shard_streams(w["streams"], rank, world)
@@ -311,192 +317,112 @@ def main():
         s_lo, s_hi = rank, rank + 1  # one stream (batch) per rank
     n_streams = s_hi - s_lo
     C = w["ch"] * (n_streams if w["scaling"] == "strong" else 1)
-    tdt = {"f32": torch.float32, "f64": torch.float64, "pcm16": torch.int16}[w["io"]]
     pcm_scale = 1.0 / 32767.0 if w["io"] == "pcm16" else None  # main.go:54, :449-460
     x_host = None
-    if args.workload == "cfg2":  # the exact generator of the round-1 line (numpy, per-channel seeds)
-        x_host = synth_stream(frames, C, 4242 + 2 * s_lo, w["ir"])
-        x = torch.from_numpy(x_host).to(dev)
-    elif pcm_scale:
-        xs = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], torch.float32)
-        x = torch.round(xs.clamp(-1, 1) * (32767 * 0.98)).to(torch.int16)
-        del xs
-    else:
-        x = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], tdt)
+    x = None
+    if not dry:
+        tdt = {"f32": torch.float32, "f64": torch.float64, "pcm16": torch.int16}[w["io"]]
+        if key == "cfg2":  # the exact generator of the round-1 line (numpy, per-channel seeds)
+            x_host = synth_stream(frames, C, 4242 + 2 * s_lo, w["ir"])
+            x = torch.from_numpy(x_host).to(dev)
+        elif pcm_scale:
+            xs = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], torch.float32)
+            x = torch.round(xs.clamp(-1, 1) * (32767 * 0.98)).to(torch.int16)
+            del xs
+        else:
+            x = synth_device(torch, frames, C, 4242 + 7919 * s_lo, w["ir"], tdt)
 
-    cfg = gar.Config(w["ir"], w["orr"], w["ch"], getattr(gar, "Quality" + w["preset"]),
-                     ComputeDtype=getattr(gar, w["compute"]), Device=dev.index)
-    r = gar.NewBatch(cfg, n_streams) if w["scaling"] == "strong" else gar.New(
-        gar.Config(w["ir"], w["orr"], C, getattr(gar, "Quality" + w["preset"]),
-                   ComputeDtype=getattr(gar, w["compute"]), Device=dev.index))
+    q = getattr(gar, "Quality" + w["preset"])
+    cd = getattr(gar, w["compute"])
+    didx = dev.index if dev is not None else 0
+    if w["scaling"] == "strong":
+        r = gar.NewBatch(gar.Config(w["ir"], w["orr"], w["ch"], q, ComputeDtype=cd, Device=didx, DryRun=dry), n_streams)
+    else:
+        r = gar.New(gar.Config(w["ir"], w["orr"], C, q, ComputeDtype=cd, Device=didx, DryRun=dry))
     chunk = w["chunk"]
-    if chunk:
-        bounds = [(s, min(chunk, frames - s)) for s in range(0, frames, chunk)]
+    bounds = [(s, min(chunk, frames - s)) for s in range(0, frames, chunk)] if chunk else [(0, frames)]
+    L = gar.lib()
+    if dry:
+        import ctypes as Ct
+        io = {"f32": gar.F32, "f64": gar.F64, "pcm16": gar.PCM16}[w["io"]]
+        nz = Ct.c_void_p(1)  # never dereferenced by a dry-run handle
+
+        def step():  # the host state machine only (no device work): exact per-call output counts
+            r.Reset()
+            o = 0
+            got = Ct.c_int64(0)
+            for _, n in bounds:
+                gar._check(L.gar_process_device(r._h, nz, io, C, 1, n, C, nz, io, C, 1, 1 << 40, Ct.byref(got), None))
+                o += got.value
+            gar._check(L.gar_flush_device(r._h, C, nz, io, C, 1, 1 << 40, Ct.byref(got), None))
+            return o, got.value
     else:
-        bounds = [(0, frames)]
-    # output bound: the exact total depends on the carried phase, so allocate ratio*frames + slack
-    n_out = int(frames * w["orr"] / w["ir"]) + 64 * (len(bounds) + 1)
-    y = torch.empty((n_out, C), dtype=tdt, device=dev)
-    yf = torch.empty((max(gar.lib().gar_device_flush_size(r._h), 1) + 4096, C), dtype=tdt, device=dev)
+        # output bound: the exact total depends on the carried phase, so allocate ratio*frames + slack
+        n_out = int(frames * w["orr"] / w["ir"]) + 64 * (len(bounds) + 1)
+        y = torch.empty((n_out, C), dtype=tdt, device=dev)
+        yf = torch.empty((max(L.gar_device_flush_size(r._h), 1) + 4096, C), dtype=tdt, device=dev)
 
-    def step():
-        r.Reset()
-        o = 0
-        for s, n in bounds:
-            o += r.process_device(x[s:s + n], out=y[o:]).shape[0]
-        tail = r.flush_device(out=yf)
-        return o, tail.shape[0]
+        def step():
+            r.Reset()
+            o = 0
+            for s, n in bounds:
+                o += r.process_device(x[s:s + n], out=y[o:]).shape[0]
+            tail = r.flush_device(out=yf)
+            return o, tail.shape[0]
 
-    inline_prof = os.environ.get("GAR_BENCH_PROF_INLINE", "1") == "1"
-    for _ in range(args.warmup):
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    inline_prof = os.environ.get("GAR_BENCH_PROF_INLINE", "1") == "1" and not dry
+    for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if inline_prof:  # HIP events around every launch inside the timed region (on the launch stream)
         r.profile(True)
         for k in range(6):
             r.profile_read(k)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    barrier()
+    sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         n_proc, n_tail = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    sync()
+    barrier()
     t1 = time.perf_counter()
-    if not inline_prof:  # development: a separate profiled pass (the timed steps carry no event packets)
+    if not dry and not inline_prof:  # development: a separate profiled pass (the timed steps carry no event packets)
         r.profile(True)
         for k in range(6):
             r.profile_read(k)
-        for _ in range(args.steps):
+        for _ in range(steps):
             step()
-        torch.cuda.synchronize()
-    prof = {k: r.profile_read(k) for k in range(6)}
-    r.profile(False)
+        sync()
+    prof = {k: (r.profile_read(k) if not dry else (0.0, 0)) for k in range(6)}
+    if not dry:
+        r.profile(False)
 
-    local_samples = frames * C * args.steps
-    elapsed, total_samples = reduce_stats(t1 - t0, local_samples, dev)
+    local_samples = frames * C * steps
+    elapsed, total_samples = reduce_stats(t1 - t0, local_samples, dev if not dry else None)
+    _, total_out = reduce_stats(0.0, (n_proc + n_tail) * C, dev if not dry else None)
 
-    # parity vs the CPU oracle (rank 0): a prefix of the first and last channels, and a
-    # suffix (the last seconds of Process + the whole Flush tail) for single-stage designs
-    rms = None
-    rms_tail = None
-    if rank == 0 and args.check_seconds > 0:
-        from oracle import oracle as O
-        O.build()
-        preset = getattr(O, "P_" + w["preset"].upper())
-        m = min(frames, int(args.check_seconds * w["ir"]))
-        got = y[:n_proc].double().cpu().numpy()
-        if pcm_scale:  # PCM: both sides in full-scale units (the oracle is fed the kernel's f32 inputs)
-            got = got * pcm_scale
+    rms, rms_tail = None, None
+    check_s = args.check_seconds if primary else min(args.check_seconds, 2.0)
+    if rank == 0 and check_s > 0 and not dry:
+        rms, rms_tail = oracle_check(w, key, gar, x, x_host, y, yf, n_proc, n_tail, frames, C, check_s, pcm_scale)
 
-        def xin(a):
-            a = np.asarray(a, dtype=np.float64)
-            return (a * pcm_scale).astype(np.float32).astype(np.float64) if pcm_scale else a
-        chans = sorted({0, C - 1})
-        errs = []
-        for c in chans:
-            xc = xin(x_host[:m, c] if x_host is not None else x[:m, c].cpu().numpy())
-            ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
-            want = ref.process(xc, 0)
-            errs.append(np.mean((got[: len(want), c] - want) ** 2))
-        rms = float(np.sqrt(np.mean(errs)))
-        # suffix: a single-stage fused design repeats every Qc inputs / Pc outputs, so the oracle
-        # restarted at input m0 = k*Qc reproduces outputs k*Pc + j once its transient has passed
-        geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), ENGINE_Q[w["preset"]](gar))
-        stages = O.NewResampler(w["ir"], w["orr"], 1, preset).stages()[1]
-        if len(stages) == 1 and geom.fused:
-            Qc, Pc = geom.fir_period_in, geom.fir_period_out
-            k = max(0, (frames - m) // Qc)
-            m0 = k * Qc
-            skip = 4 * geom.fir_taps_max
-            tail = yf[:n_tail].double().cpu().numpy() * (pcm_scale or 1.0)
-            errs = []
-            for c in chans:
-                xc = xin(x_host[m0:, c] if x_host is not None else x[m0:, c].cpu().numpy())
-                ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
-                want = np.concatenate([ref.process(xc, 0), ref.flush(0)])
-                full = np.concatenate([got[k * Pc:, c], tail[:, c]])
-                if len(full) != len(want):
-                    errs.append(float("inf"))
-                    continue
-                errs.append(np.mean((full[skip:] - want[skip:]) ** 2))
-            rms_tail = float(np.sqrt(np.mean(errs)))
-
-    # roofline of the dominant kernel (HIP events on the launch stream, inside the library)
-    kinds = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)",
-             4: "polyphase with live cubic coefficients (poly_kernel)", 5: "QualityQuick cubic stage (cubic_kernel)"}
-    dom = max((0, 1, 2, 4, 5), key=lambda k: prof[k][0])
-    kms, launches = prof[dom]
-    launch_s = (kms / 1e3) / max(launches, 1)
-    in_bytes = {"f32": 4, "f64": 8, "pcm16": 2}[w["io"]]
-    out_samples_step = (n_proc + n_tail) * C
-    if w["compute"] == "F32" and dom in w.get("kind_bytes", {}):
-        # that stage's own stream bytes per input frame and channel (its input read once, output written once)
-        algo_bytes = w["kind_bytes"][dom] * frames * C
-        algo_per_launch = algo_bytes / max(launches / args.steps, 1)
-        achieved = algo_per_launch / launch_s / 1e9 if launches else None
-        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
-                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
-        kernel_keys = ["poly_kernel"] if dom == 4 else ["cubic_kernel"]
-        kname = kinds[dom]
-        algo_unit_bytes = algo_per_launch
-    elif w["compute"] == "F32":
-        # HBM-bound streaming FIR: algorithmic bytes = input read once + output written once
-        algo_bytes = frames * C * in_bytes + n_proc * C * in_bytes
-        algo_per_launch = algo_bytes / max(launches / args.steps, 1)
-        achieved = algo_per_launch / launch_s / 1e9 if launches else None
-        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
-                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
-        kernel_keys = ["hxs_kernel", "hx_kernel"]
-        kname = ("hxs_kernel / hx_kernel (fused DFTx2->polyphase banded FIR, f16-split "
-                 "v_mfma_f32_16x16x32_f16, f32 accumulation)")
-        algo_unit_bytes = algo_per_launch
-    else:
-        # f64: MFMA-bound (f64 matrix rate); useful flops of the dominant stage
-        if dom == 2:
-            flops_step = 2.0 * DECIM_MACS_PER_INPUT * frames * C
-        else:
-            geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), ENGINE_Q[w["preset"]](gar))
-            flops_step = 2.0 * geom.useful_macs_per_output * out_samples_step
-        fl_launch = flops_step / max(launches / args.steps, 1)
-        achieved = fl_launch / launch_s / 1e12 if launches else None
-        roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
-                "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
-        kernel_keys = ["bg_kernel"]
-        kname = f"bg_kernel<double> ({kinds[dom]}, v_mfma_f64_16x16x4_f64)"
-        algo_unit_bytes = None
-    roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[args.workload]
-    roof["kernel_ms_by_kind"] = {kinds[k]: round(prof[k][0] / args.steps, 4) for k in prof if prof[k][1]}
-    roof.update({"traffic": None, "kernel": kname, "kernel_kind": kinds[dom],
-                 "kernel_ms_per_launch": round(launch_s * 1e3, 5), "launches": launches})
-    if algo_unit_bytes:
-        roof["algo_hbm_bytes_per_launch"] = int(algo_unit_bytes)
-        roof["algo_bytes_per_input_sample"] = round(algo_unit_bytes * launches / args.steps / (frames * C), 3)
-    if args.workload in ("cfg2", "ns256", "cfg4"):
-        geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), gar.Engine24Bit)
-        useful = geom.useful_macs_per_output
-        roof["useful_macs_per_output"] = round(useful, 2)
-        outs_launch = n_proc * C / max(launches / args.steps, 1)
-        roof["mfma_tflops_f16"] = round(2.0 * 3 * useful * outs_launch / launch_s / 1e12, 2) if launches else None
-        roof["mfma_peak_tflops_f16"] = PEAK_F16_MATRIX_TFLOPS
-
-    # streaming drop-in usage (rank 0): 4096-frame (cfg5: 4800) chunks through the device
-    # API and through the host C-ABI (ProcessMulti over planar float64, the cgo shim's call)
-    streaming = None
-    if rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak" and w["io"] == "f32":
-        streaming = time_streaming(gar, torch, w, x, C, dev)
-
-    line = {
-        "metric": metric_for(args.workload, w),
+    obj = {
+        "metric": metric_for(key, w),
         "value": round(total_samples / elapsed / 1e6, 2),
         "unit": "Msamples/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": w["scaling"],
         "vs_baseline": None,
@@ -515,31 +441,228 @@ def main():
             "parallelism": (f"{w['streams']} streams sharded over {world} GPUs" if w["scaling"] == "strong"
                             else f"independent streams, 1 per GPU x {world}"),
         },
-        "roofline": roof,
-        "arith": (("int16 PCM I/O converted in the kernel's loads (float64(i)/32767 -> f32) and stores "
-                   "(clamp, x32767, truncate); rms_vs_oracle in full-scale units includes the output "
-                   "quantization (~0.6 LSB = 1.8e-5); " if pcm_scale else "f32 I/O; ") +
-                  "products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
-                  "(error at the level of exact-f32 arithmetic)" if w["compute"] == "F32"
-                  else "f64 I/O and f64 MFMA (v_mfma_f64_16x16x4_f64)"),
-        "streaming": streaming,
-        "cpu_baseline": None,
+        "output_samples_total": int(total_out),
+        "input_samples_total": int(total_samples / steps),
     }
-    if rank == 0 and world == 1 and not args.no_pmc:
-        traffic, err = pmc_traffic(args, kernel_keys)
-        if traffic:
-            per_launch = traffic["bytes"]
-            line["roofline"]["traffic"] = per_launch
-            line["roofline"]["traffic_read"] = traffic["read_bytes"]
-            line["roofline"]["traffic_write"] = traffic["write_bytes"]
+    kernel_keys = []
+    if not dry:
+        roof, kernel_keys = roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail)
+        obj["roofline"] = roof
+        obj["arith"] = (("int16 PCM I/O converted in the kernel's loads (float64(i)/32767 -> f32) and stores "
+                         "(clamp, x32767, truncate); rms_vs_oracle in full-scale units includes the output "
+                         "quantization (~0.6 LSB = 1.8e-5); " if pcm_scale else "f32 I/O; ") +
+                        "products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
+                        "(error at the level of exact-f32 arithmetic)" if w["compute"] == "F32"
+                        else "f64 I/O and f64 MFMA (v_mfma_f64_16x16x4_f64)")
+        if primary and rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak" \
+                and w["io"] == "f32":
+            obj["streaming"] = time_streaming(gar, torch, w, x, C, dev)
+        del x, y, yf
+    del r
+    if not dry:
+        torch.cuda.empty_cache()
+    return obj, kernel_keys
+
+
+def oracle_check(w, key, gar, x, x_host, y, yf, n_proc, n_tail, frames, C, check_s, pcm_scale):
+    """Parity vs the CPU oracle (rank 0, after the timed region): a prefix of the first and last
+    channels, and a suffix (the last seconds of Process + the whole Flush tail) for single-stage
+    fused designs."""
+    from oracle import oracle as O
+    O.build()
+    preset = getattr(O, "P_" + w["preset"].upper())
+    m = min(frames, int(check_s * w["ir"]))
+    got = y[:n_proc].double().cpu().numpy()
+    if pcm_scale:  # PCM: both sides in full-scale units (the oracle is fed the kernel's f32 inputs)
+        got = got * pcm_scale
+
+    def xin(a):
+        a = np.asarray(a, dtype=np.float64)
+        return (a * pcm_scale).astype(np.float32).astype(np.float64) if pcm_scale else a
+    chans = sorted({0, C - 1})
+    errs = []
+    for c in chans:
+        xc = xin(x_host[:m, c] if x_host is not None else x[:m, c].cpu().numpy())
+        ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
+        want = ref.process(xc, 0)
+        errs.append(np.mean((got[: len(want), c] - want) ** 2))
+    rms = float(np.sqrt(np.mean(errs)))
+    rms_tail = None
+    # suffix: a single-stage fused design repeats every Qc inputs / Pc outputs, so the oracle
+    # restarted at input m0 = k*Qc reproduces outputs k*Pc + j once its transient has passed
+    geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), ENGINE_Q[w["preset"]](gar))
+    stages = O.NewResampler(w["ir"], w["orr"], 1, preset).stages()[1]
+    if len(stages) == 1 and geom.fused and w["streams"] == 1:
+        Qc, Pc = geom.fir_period_in, geom.fir_period_out
+        k = max(0, (frames - m) // Qc)
+        m0 = k * Qc
+        skip = 4 * geom.fir_taps_max
+        tail = yf[:n_tail].double().cpu().numpy() * (pcm_scale or 1.0)
+        errs = []
+        for c in chans:
+            xc = xin(x_host[m0:, c] if x_host is not None else x[m0:, c].cpu().numpy())
+            ref = O.NewResampler(w["ir"], w["orr"], 1, preset)
+            want = np.concatenate([ref.process(xc, 0), ref.flush(0)])
+            full = np.concatenate([got[k * Pc:, c], tail[:, c]])
+            if len(full) != len(want):
+                errs.append(float("inf"))
+                continue
+            errs.append(np.mean((full[skip:] - want[skip:]) ** 2))
+        rms_tail = float(np.sqrt(np.mean(errs)))
+    return rms, rms_tail
+
+
+def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
+    """Roofline object of the dominant kernel kind (HIP events on the launch stream, inside the
+    library): algorithmic bytes (HBM-bound f32 FIR) or useful flops (MFMA-bound f64) of the
+    stage that kind runs, per launch, over the average launch time."""
+    dom = max((0, 1, 2, 4, 5), key=lambda k: prof[k][0])
+    kms, launches = prof[dom]
+    launch_s = (kms / 1e3) / max(launches, 1)
+    per_step = max(launches / steps, 1)
+    in_bytes = {"f32": 4, "f64": 8, "pcm16": 2}[w["io"]]
+    # the pipeline stage the dominant kind runs, and its input/output samples per step
+    nst = r.num_stages()
+    geoms = [r.stage_geometry(j) for j in range(nst)]
+    sidx = next((j for j in range(nst) if geoms[j][1].kind in KIND_STAGE[dom]), nst - 1)
+    ratio_in = 1.0
+    for j in range(sidx):
+        ratio_in *= geoms[j][0]
+    st_ratio, st_geom = geoms[sidx]
+    st_in = frames * C * ratio_in
+    st_out = (n_proc + n_tail) * C if sidx == nst - 1 else st_in * st_ratio
+    if w["compute"] == "F32" and dom in w.get("kind_bytes", {}):
+        # that stage's own stream bytes per input frame and channel (its input read once, output written once)
+        algo_per_launch = w["kind_bytes"][dom] * frames * C / per_step
+        achieved = algo_per_launch / launch_s / 1e9 if launches else None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
+        kernel_keys = ["poly_kernel"] if dom == 4 else ["cubic_kernel"]
+        kname = KIND_NAMES[dom]
+        algo_unit_bytes = algo_per_launch
+    elif w["compute"] == "F32":
+        # HBM-bound streaming FIR: algorithmic bytes = input read once + output written once
+        algo_per_launch = (frames * C * in_bytes + n_proc * C * in_bytes) / per_step
+        achieved = algo_per_launch / launch_s / 1e9 if launches else None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
+                "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
+        kernel_keys = ["hxs_kernel", "hx_kernel"]
+        kname = ("hxs_kernel / hx_kernel (fused DFTx2->polyphase banded FIR, f16-split "
+                 "v_mfma_f32_16x16x32_f16, f32 accumulation)")
+        algo_unit_bytes = algo_per_launch
+    else:
+        # f64: MFMA-bound (f64 matrix rate); useful flops of the dominant stage's own design
+        flops_step = 2.0 * st_geom.useful_macs_per_output * st_out
+        fl_launch = flops_step / per_step
+        achieved = fl_launch / launch_s / 1e12 if launches else None
+        roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
+                "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
+        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel"]
+        kname = (f"{'poly_kernel<double>' if dom == 4 else 'bg_kernel<double>'} ({KIND_NAMES[dom]}, stage {sidx}: "
+                 f"{48000:g}->{48000 * st_ratio:g} Hz engine, v_mfma_f64_16x16x4_f64)")
+        algo_unit_bytes = (st_in + st_out) * 8 / per_step
+        roof["useful_macs_per_output"] = round(st_geom.useful_macs_per_output, 2)
+        roof["stage_outputs_per_step"] = int(st_out)
+    roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[key]
+    roof["kernel_ms_by_kind"] = {KIND_NAMES[k]: round(prof[k][0] / steps, 4) for k in prof if prof[k][1]}
+    roof["launches_per_step_by_kind"] = {KIND_NAMES[k]: prof[k][1] / steps for k in prof if prof[k][1]}
+    roof.update({"traffic": None, "kernel": kname, "kernel_kind": KIND_NAMES[dom],
+                 "kernel_ms_per_launch": round(launch_s * 1e3, 5), "launches": launches})
+    if algo_unit_bytes:
+        roof["algo_hbm_bytes_per_launch"] = int(algo_unit_bytes)
+        roof["algo_bytes_per_input_sample"] = round(algo_unit_bytes * per_step / (frames * C), 3)
+    if key in ("cfg2", "ns256", "cfg4"):
+        geom, _ = gar.design_engine(48000.0, 48000.0 * (w["orr"] / w["ir"]), gar.Engine24Bit)
+        useful = geom.useful_macs_per_output
+        roof["useful_macs_per_output"] = round(useful, 2)
+        outs_launch = n_proc * C / per_step
+        roof["mfma_tflops_f16"] = round(2.0 * 3 * useful * outs_launch / launch_s / 1e12, 2) if launches else None
+        roof["mfma_peak_tflops_f16"] = PEAK_F16_MATRIX_TFLOPS
+    return roof, kernel_keys
+
+
+def attach_traffic(obj, args, key, kernel_keys):
+    """Live PMC traffic of the dominant kernel (world 1); refused when the selected dispatch
+    reports fewer bytes than the algorithmic ones (a wrong dispatch or a missed launch)."""
+    roof = obj.get("roofline")
+    if not roof or not kernel_keys:
+        return
+    traffic, err = pmc_traffic(args, key, kernel_keys)
+    if not traffic:
+        roof["traffic_error"] = err
+        return
+    algo = roof.get("algo_hbm_bytes_per_launch")
+    if algo and traffic["bytes"] < 0.9 * algo:
+        roof["traffic_error"] = (f"selected dispatch reports {traffic['bytes']:.4g} B < algorithmic {algo:.4g} B "
+                                 f"(wrong or missed dispatch): not published")
+        roof["traffic_rejected"] = traffic
+        return
+    roof["traffic"] = traffic["bytes"]
+    roof["traffic_read"] = traffic["read_bytes"]
+    roof["traffic_write"] = traffic["write_bytes"]
+    roof["traffic_fetch_correction"] = traffic["fetch_correction"]
+    if algo:
+        roof["traffic_over_algo"] = round(traffic["bytes"] / algo, 4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--seconds", type=float, default=None, help="stream length override (primary workload)")
+    ap.add_argument("--secondary", default="auto",
+                    help="comma list of workloads timed beside the primary line, 'auto' or 'none'")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live PMC traffic passes")
+    ap.add_argument("--no-streaming", action="store_true", help="skip the chunked drop-in timing")
+    ap.add_argument("--check-seconds", type=float, default=5.0, help="prefix (and suffix) checked against the oracle")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: dry-run handles (exact host state machine) over gloo -- the multi-rank "
+                         "sharding and reduction end to end on CPU (tests/test_dist.py)")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    dev = None
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group(backend="gloo")
+    else:
+        import torch
+        if world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
         else:
-            line["roofline"]["traffic_error"] = err
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(w)
+            torch.cuda.set_device(0)
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+    line, keys = run_workload(args.workload, args, args.steps, args.warmup, world, rank, dev, primary=True)
+    if rank == 0 and world == 1 and not args.no_pmc and not args.dry_run:
+        attach_traffic(line, args, args.workload, keys)
+    line["cpu_baseline"] = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        line["cpu_baseline"] = cpu_baseline(WORKLOADS[args.workload])
+    sec = (secondary_default(args.workload, world) if args.secondary == "auto"
+           else [] if args.secondary == "none" else [k for k in args.secondary.split(",") if k])
+    if sec:
+        line["secondary"] = {}
+        for key in sec:
+            obj, keys = run_workload(key, args, min(args.steps, 10), min(args.warmup, 2), world, rank, dev,
+                                     primary=False)
+            if rank == 0 and world == 1 and not args.no_pmc and not args.dry_run:
+                attach_traffic(obj, args, key, keys)
+            line["secondary"][key] = obj
+    if args.dry_run:
+        line["dry_run"] = True
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
-        torch.distributed.destroy_process_group()
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def time_streaming(gar, torch, w, x, C, dev, seconds=60.0):

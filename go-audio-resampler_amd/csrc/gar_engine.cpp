@@ -143,6 +143,7 @@ bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry, const
             d.dftC = static_cast<const double*>(h.banks2.p);
         }
     }
+    d.hxsOk = hxsPlanFits(d) ? 1 : 0;  // PCM stores/loads fuse only into hxs_kernel (pcmFusable)
     bg.hx = &h.d;
     return true;
 }
@@ -1178,7 +1179,38 @@ bool pcmFusable(const Handle* h) {
     const StageRT& st = *h->stages[0];
     if (!st.fused || h->groups[0].cnt.empty() || h->groups[0].cnt[0].staged) return false;
     const HxDev* hx = st.fusedD.hx;
-    return hx && hx->rb && hx->nw <= kHxRbMaxWaves && hx->NS >= 1 && hx->NS <= 10;
+    return hx && hx->hxsOk;
+}
+}  // namespace
+}  // namespace gar
+
+namespace gar {
+namespace {
+void fillGeometry(const EngineDesign& d, gar_engine_geometry* geom) {
+    std::memset(geom, 0, sizeof(*geom));
+    geom->kind = static_cast<int32_t>(d.kind);
+    geom->dft_factor = d.dft.factor;
+    geom->dft_taps = d.dft.taps;
+    geom->poly_phases = d.poly.L;
+    geom->poly_taps = d.poly.taps;
+    geom->poly_step = d.poly.step;
+    geom->decim_factor = d.decim.factor;
+    geom->decim_taps = d.decim.taps;
+    FirPeriodic f;
+    bool have = false;
+    if (d.kind == EngineKind::DftPoly && firComposite(d.dft, d.poly, f)) { geom->fused = 1; have = true; }
+    else if (d.kind == EngineKind::DftOnly) { f = firFromDft(d.dft); have = true; }
+    else if (d.kind == EngineKind::Decim) { f = firFromDecim(d.decim); have = true; }
+    if (have) {
+        geom->fir_period_out = f.P;
+        geom->fir_period_in = f.Q;
+        for (const auto& row : f.rows) geom->fir_taps_max = std::max<int32_t>(geom->fir_taps_max, static_cast<int32_t>(row.size()));
+        BgPlan p;
+        if (buildBgPlan(f, false, p)) {
+            geom->useful_macs_per_output = p.usefulMacsPerOutput;
+            geom->mfma_macs_per_output = p.mfmaMacsPerOutput;
+        }
+    }
 }
 }  // namespace
 }  // namespace gar
@@ -1492,6 +1524,9 @@ void gar_reset(gar_resampler* r) {
     DeviceGuard dg(r->dry ? -1 : r->device);
     try {
         if (r->poisoned) {  // recover: drain the handle's streams, fresh state
+            // the failing call recorded no order event, and launches it already queued on a
+            // caller stream may still read the histories and scratch freed below: drain the device
+            (void)hipDeviceSynchronize();
             if (r->stream) (void)hipStreamSynchronize(r->stream);
             if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
             (void)hipGetLastError();
@@ -1538,20 +1573,26 @@ gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
     std::memset(info, 0, sizeof(*info));
     std::snprintf(info->algorithm, sizeof(info->algorithm), "%s", "multi-stage");
     info->latency = gar_get_latency(r);
-    // MemoryUsage as the reference counts it per channel (constant.go:457-466): the ring
-    // buffers between stages (default capacity 8192 float64, pipeline constants.go:55) plus each
-    // stage's coefficient tables and delay line (StageAdapter.GetMemoryUsage,
-    // stage_adapter.go:66-96); here the tables are shared by all channels on the device, but
-    // the figure keeps the reference's per-channel accounting.
-    const int64_t es = r->f64 ? 8 : 4;
-    int64_t perCh = static_cast<int64_t>(r->stages.size() + 1) * 8192 * 8;
+    // MemoryUsage as the reference counts it for a fresh handle (constant.go:457-468), per channel:
+    //  * every ring buffer's capacity in float64 -- defaultBufferSize 8192, buffer 0 sized
+    //    MaxInputSize * bufferSizeMultiplier when set (constant.go:72-78, constants.go:55-57);
+    //  * StageAdapter.GetMemoryUsage (stage_adapter.go:66-96) of each stage, whose elements are
+    //    float64 on the New path (Resampler[float64], stages.go:63): the DFT pre-stage's
+    //    factor x taps coefficients + history capacity taps * historyBufferMultiplier (2,
+    //    dft_stage.go:142), the polyphase stage's `a` bank L x taps + history capacity 2 * taps
+    //    (polyphase_stage.go:167); decimation stages are not counted.
+    // The reference's history capacities then grow with use (appendStable, polyphase.go:36-44);
+    // the device histories here are shared per group, so the figure stays the fresh one.
+    const int64_t es = 8;
+    int64_t perCh = 0;
+    for (size_t j = 0; j <= r->stages.size(); ++j)
+        perCh += (j == 0 && r->cfg.max_input_size > 0 ? r->cfg.max_input_size * 2 : 8192) * 8;
     for (const auto& s : r->stages) {
         const EngineDesign& d = s->d;
         if ((d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) && d.dft.factor > 1)
-            perCh += static_cast<int64_t>(d.dft.factor) * d.dft.taps * es + static_cast<int64_t>(d.dft.taps) * es;
+            perCh += static_cast<int64_t>(d.dft.factor) * d.dft.taps * es + 2 * static_cast<int64_t>(d.dft.taps) * es;
         if (d.kind == EngineKind::DftPoly)
-            perCh += 4 * static_cast<int64_t>(d.poly.L) * d.poly.taps * es + static_cast<int64_t>(d.poly.taps) * es;
-        if (d.kind == EngineKind::Decim) perCh += 2 * static_cast<int64_t>(d.decim.taps) * es;
+            perCh += static_cast<int64_t>(d.poly.L) * d.poly.taps * es + 2 * static_cast<int64_t>(d.poly.taps) * es;
     }
     info->memory_usage = perCh * r->channels;
     if (!r->stages.empty()) {
@@ -1595,6 +1636,26 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
     r->profile = on != 0;
 }
 
+gar_status gar_stage_state(const gar_resampler* r, int32_t stage, int32_t* fused_plan, int32_t* fused_now) {
+    if (!r || !fused_plan || !fused_now || stage < 0 || stage >= static_cast<int32_t>(r->stages.size()))
+        return GAR_ERR_INVALID_ARGUMENT;
+    const gar::StageRT& st = *r->stages[stage];
+    *fused_plan = st.fused ? 1 : 0;
+    const gar::Group* g = r->groups.empty() ? nullptr : &r->groups[0];
+    *fused_now = (st.fused && g && !g->cnt[stage].staged) ? 1 : 0;
+    return GAR_OK;
+}
+
+gar_status gar_stage_geometry(const gar_resampler* r, int32_t stage, double* stage_ratio, gar_engine_geometry* geom) {
+    if (!r || !geom || stage < 0 || stage >= static_cast<int32_t>(r->stages.size())) return GAR_ERR_INVALID_ARGUMENT;
+    const gar::EngineDesign& d = r->stages[stage]->d;
+    fillGeometry(d, geom);
+    if (stage_ratio) *stage_ratio = d.ratio;
+    return GAR_OK;
+}
+
+int32_t gar_num_stages(const gar_resampler* r) { return r ? static_cast<int32_t>(r->stages.size()) : 0; }
+
 gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t* launches) {
     if (!r || kind < 0 || kind > 5) return GAR_ERR_INVALID_ARGUMENT;
     DeviceGuard dg(r->dry ? -1 : r->device);
@@ -1621,32 +1682,7 @@ gar_status gar_design_engine(double in_rate, double out_rate, int32_t q, gar_eng
     EngineDesign d;
     std::string err;
     if (!designEngine(in_rate, out_rate, static_cast<Quality>(q), d, err)) return guard(GAR_ERR_INVALID_CONFIG, err.c_str());
-    if (geom) {
-        std::memset(geom, 0, sizeof(*geom));
-        geom->kind = static_cast<int32_t>(d.kind);
-        geom->dft_factor = d.dft.factor;
-        geom->dft_taps = d.dft.taps;
-        geom->poly_phases = d.poly.L;
-        geom->poly_taps = d.poly.taps;
-        geom->poly_step = d.poly.step;
-        geom->decim_factor = d.decim.factor;
-        geom->decim_taps = d.decim.taps;
-        FirPeriodic f;
-        bool have = false;
-        if (d.kind == EngineKind::DftPoly && firComposite(d.dft, d.poly, f)) { geom->fused = 1; have = true; }
-        else if (d.kind == EngineKind::DftOnly) { f = firFromDft(d.dft); have = true; }
-        else if (d.kind == EngineKind::Decim) { f = firFromDecim(d.decim); have = true; }
-        if (have) {
-            geom->fir_period_out = f.P;
-            geom->fir_period_in = f.Q;
-            for (const auto& row : f.rows) geom->fir_taps_max = std::max<int32_t>(geom->fir_taps_max, static_cast<int32_t>(row.size()));
-            BgPlan p;
-            if (buildBgPlan(f, false, p)) {
-                geom->useful_macs_per_output = p.usefulMacsPerOutput;
-                geom->mfma_macs_per_output = p.mfmaMacsPerOutput;
-            }
-        }
-    }
+    if (geom) fillGeometry(d, geom);
     if (dft && !d.dft.c.empty()) std::memcpy(dft, d.dft.c.data(), d.dft.c.size() * 8);
     if (pa && !d.poly.a.empty()) std::memcpy(pa, d.poly.a.data(), d.poly.a.size() * 8);
     if (pb && !d.poly.b.empty()) std::memcpy(pb, d.poly.b.data(), d.poly.b.size() * 8);

@@ -82,6 +82,27 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 // LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B).
 static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256; }
 
+// Ring geometry of G periods per group: R ring rows, Rt rows incl. the mirror (rounded to 16 so
+// the quad stride 16*Rt + 64 is 64 mod 256 B: the four quads of a transposed read land on
+// distinct banks), Wg rows one group reads.
+static void hxsRingFor(const HxDev& p, int G, int& R, int& Rt, int& Wg) {
+    const int GQ = G * p.Qc;
+    Wg = (G - 1) * p.Qc + p.Kread;
+    const int n = (Wg + GQ + GQ - 1) / GQ;
+    R = n * GQ;
+    Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
+}
+static bool hxsRingFits(const HxDev& p, int G, int Rt) {
+    return hxsLds(Rt) <= 160 * 1024 && (G * p.Qc + 63) / 64 <= kHxsNP;
+}
+
+bool hxsPlanFits(const HxDev& p) {
+    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return false;
+    int R, Rt, Wg;
+    hxsRingFor(p, 1, R, Rt, Wg);
+    return hxsRingFits(p, 1, Rt);
+}
+
 // hipErrorNotSupported: the plan does not fit this kernel's geometry (the caller uses hx_kernel).
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
@@ -121,15 +142,6 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     if (ncols > (int64_t(1) << 30) || Np > (int64_t(1) << 24)) return hipErrorNotSupported;
 
     // group size: largest G <= kHxsMaxG that fits the LDS ring and the loaders' registers, not above Np
-    auto ringFor = [&](int G, int& R, int& Rt, int& Wg) {
-        const int GQ = G * static_cast<int>(Qc);
-        Wg = (G - 1) * static_cast<int>(Qc) + p.Kread;
-        const int n = (Wg + GQ + GQ - 1) / GQ;
-        R = n * GQ;
-        // rows incl. the mirror, rounded to 16 so the quad stride 16*Rt + 64 is 64 mod 256 B:
-        // the four quads of a transposed read land on distinct banks
-        Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
-    };
     // load layout: STEREO frames (two chunks per quad, dwordx2), ROW16 (four channels per quad,
     // dwordx4), or gathered at conversion time for any other layout
     const uintptr_t inA = reinterpret_cast<uintptr_t>(src.in);
@@ -145,17 +157,13 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     } else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) {
         fmt = 2;
     }
-    auto fits = [&](int G, int Rt) {
-        const int GQ = G * static_cast<int>(Qc);
-        return hxsLds(Rt) <= 160 * 1024 && (GQ + 63) / 64 <= kHxsNP;
-    };
     int G = 0, R = 0, Rt = 0, Wg = 0;
     for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
         int r, rt, wg;
-        ringFor(cand, r, rt, wg);
+        hxsRingFor(p, cand, r, rt, wg);
         if (cand > 1 && cand > Np) continue;
         if (knobG > 0 && cand > knobG && cand > 1) continue;
-        if (!fits(cand, rt)) continue;
+        if (!hxsRingFits(p, cand, rt)) continue;
         G = cand; R = r; Rt = rt; Wg = wg;
         break;
     }

@@ -628,10 +628,11 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             hxsBarrier();  // step done: load j in the ring, load j + 1 landed
             if (x.prof) { tm += t1 - t0; tw += __builtin_amdgcn_s_memtime() - t1; }
         }
-        if (*sh_.flag) {  // uniform (LDS after the barrier)
+        if (*sh_.flag) {  // uniform (LDS after the barrier; reset only after the barrier below)
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
             __syncthreads();
             hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
+            __syncthreads();  // every wave's fixup read loudLo/loudHi before the next block resets them
         }
     }
     if (x.prof && lane == 0) {
@@ -691,10 +692,11 @@ __device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared
                 hxsBarrier();  // step done: load j in the ring
             }
         }
-        if (*sh_.flag) {
+        if (*sh_.flag) {  // same sequence as the compute waves
             __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
             hxsFixup(hxsCold(), b, sh_.loudLo, sh_.loudHi);
+            __syncthreads();
         }
     }
 }

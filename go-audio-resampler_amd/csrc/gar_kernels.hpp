@@ -81,6 +81,7 @@ struct HxDev {
     const double* dftC;  // [2][T1]
     int* fix;            // [1 + fixCap]: interior blocks holding loud elements (count first)
     int fixCap;
+    int hxsOk;           // host: the plan fits hxs_kernel (hxsPlanFits), so fused PCM I/O can use it
 };
 
 // General polyphase stage with live cubic coefficient interpolation
@@ -115,6 +116,9 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int 
                     HistCopy* hc = nullptr);
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
                     HistCopy* hc = nullptr);
+// True when a row-block plan fits launchHxs's geometry at one period per group (its smallest
+// ring), i.e. launchHxs never returns hipErrorNotSupported for it (gar_hxs.hip).
+bool hxsPlanFits(const HxDev& p);
 // Streaming wave-specialised variant of launchHx for row-block plans (gar_hxs.hip).
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
                      HistCopy* hc = nullptr);

@@ -198,34 +198,22 @@ std::vector<int> BgPlan::redTable() const {
     return t;
 }
 
-bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
-    if (f.P <= 0 || f.Q <= 0) return false;
-    // Pick the macro period (multiple of the FIR period) with the best
-    // useful/executed MAC ratio; prefer >= 16 rows so row blocks are full.
-    int bestMp = 1;
-    double bestEff = -1;
-    for (int mp = 1; mp <= 64; ++mp) {
-        const int Pc = f.P * mp;
-        if (Pc > 320) break;
-        double eff;
-        geomFor(f, mp, eff);
-        if (Pc < 16) eff *= static_cast<double>(Pc) / 16.0;  // partially filled row block
-        if (eff > bestEff + 1e-9) { bestEff = eff; bestMp = mp; }
-    }
+namespace {
+// Wave programs for macro period mp (waves per column group nw, column groups ncg) minimising
+// the critical SIMD's MFMA steps per column:
+//   ceil(waves/4) * kch*NS / (16 * ncg), x latency factor for < 3 waves/SIMD
+// (a program longer than maxNS runs as kch chunks of NS steps).  False when no split fits
+// the segment / reduction-slot / register limits.
+bool planPrograms(const FirPeriodic& f, bool f64, int mp, BgPlan& plan) {
     double eff;
-    const std::vector<RbGeom> rbs = geomFor(f, bestMp, eff);
+    const std::vector<RbGeom> rbs = geomFor(f, mp, eff);
     plan = BgPlan();
     plan.f64 = f64;
-    plan.P = f.P; plan.Q = f.Q; plan.mp = bestMp;
-    plan.Pc = f.P * bestMp;
-    plan.Qc = f.Q * bestMp;
+    plan.P = f.P; plan.Q = f.Q; plan.mp = mp;
+    plan.Pc = f.P * mp;
+    plan.Qc = f.Q * mp;
     plan.nrb = static_cast<int>(rbs.size());
     for (const auto& r : rbs) plan.Kc = std::max(plan.Kc, r.klo + 4 * r.nsteps);
-
-    // Choose waves per column group (nw) and column groups (ncg) minimising
-    // the critical SIMD's MFMA steps per column:
-    //   ceil(waves/4) * kch*NS / (16 * ncg), x latency factor for < 3 waves/SIMD
-    // (a program longer than maxNS runs as kch chunks of NS steps).
     const int maxNS = f64 ? 48 : 96;
     double bestCost = 1e300;
     for (int nw = 1; nw <= 16; ++nw) {
@@ -254,7 +242,31 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
             }
         }
     }
-    if (plan.progs.empty()) return false;
+    return !plan.progs.empty();
+}
+}  // namespace
+
+bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
+    if (f.P <= 0 || f.Q <= 0) return false;
+    // Macro period (multiple of the FIR period) with the best useful/executed MAC ratio among
+    // those whose programs fit (prefer >= 16 rows so row blocks are full).  A long period of a
+    // long f64 filter (48k->44.1k Q32: Pc = 294, 19 row blocks x 78 steps) can need more
+    // segments per program than kBgMaxSeg at the f64 register budget; a shorter one fits.
+    std::vector<std::pair<double, int>> cand;
+    for (int mp = 1; mp <= 64; ++mp) {
+        const int Pc = f.P * mp;
+        if (Pc > 320) break;
+        double eff;
+        geomFor(f, mp, eff);
+        if (Pc < 16) eff *= static_cast<double>(Pc) / 16.0;  // partially filled row block
+        cand.push_back({-eff, mp});
+    }
+    std::stable_sort(cand.begin(), cand.end(),
+                     [](const std::pair<double, int>& a, const std::pair<double, int>& b) { return a.first < b.first - 1e-9; });
+    bool ok = false;
+    for (const auto& c : cand)
+        if ((ok = planPrograms(f, f64, c.second, plan))) break;
+    if (!ok) return false;
 
     const size_t np = plan.progs.size();
     const int plen = plan.kch * plan.NS;  // steps per program incl. padding
@@ -286,8 +298,8 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     double useful = 0;
     for (const auto& r : f.rows) useful += static_cast<double>(r.size());
     plan.usefulMacsPerOutput = useful / f.P;
-    double exec = 0;
-    for (const auto& r : rbs) exec += 16.0 * 4.0 * r.nsteps;  // per column per macro period
+    double eff, exec = 0;
+    for (const auto& r : geomFor(f, plan.mp, eff)) exec += 16.0 * 4.0 * r.nsteps;  // per column per macro period
     plan.mfmaMacsPerOutput = exec / plan.Pc;
     return true;
 }

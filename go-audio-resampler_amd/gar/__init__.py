@@ -89,7 +89,7 @@ EXPORTED = [
     "gar_flush_multi_f64", "gar_process_device", "gar_flush_device", "gar_device_output_size",
     "gar_device_flush_size", "gar_reset", "gar_get_ratio", "gar_get_latency", "gar_get_info", "gar_channels",
     "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite", "gar_profile_enable",
-    "gar_profile_read",
+    "gar_profile_read", "gar_stage_state", "gar_num_stages", "gar_stage_geometry",
 ]
 
 _lib = None
@@ -147,6 +147,9 @@ def lib():
         "gar_design_composite": (i32, [d, d, i32, vp, vp]),
         "gar_profile_enable": (None, [vp, i32]),
         "gar_profile_read": (i32, [vp, i32, C.POINTER(d), C.POINTER(i64)]),
+        "gar_stage_state": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32)]),
+        "gar_num_stages": (i32, [vp]),
+        "gar_stage_geometry": (i32, [vp, i32, C.POINTER(d), C.POINTER(EngineGeometry)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -292,6 +295,21 @@ class Resampler:
         ms, n = C.c_double(0), C.c_int64(0)
         _check(lib().gar_profile_read(self._h, kind, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def num_stages(self):
+        return lib().gar_num_stages(self._h)
+
+    def stage_geometry(self, stage):
+        """(engine ratio, EngineGeometry) of pipeline stage `stage`."""
+        ratio, g = C.c_double(0), EngineGeometry()
+        _check(lib().gar_stage_geometry(self._h, stage, C.byref(ratio), C.byref(g)))
+        return ratio.value, g
+
+    def stage_state(self, stage):
+        """(fused_plan, fused_now) of pipeline stage `stage` (channel 0's group)."""
+        a, b = C.c_int32(0), C.c_int32(0)
+        _check(lib().gar_stage_state(self._h, stage, C.byref(a), C.byref(b)))
+        return bool(a.value), bool(b.value)
 
     @property
     def Channels(self):

@@ -195,6 +195,11 @@ void gar_profile_enable(gar_resampler *r, int32_t on);
  * flush, 4 polyphase stage with live cubic coefficients, 5 QualityQuick cubic
  * stage) since its last read. */
 gar_status gar_profile_read(gar_resampler *r, int32_t kind, double *ms, int64_t *launches);
+/* Execution mode of pipeline stage `stage` of channel 0's group: *fused_plan = 1 when the
+ * stage's DFT x2 + polyphase pair has a composite MFMA plan, *fused_now = 1 while the stream
+ * still runs on it (0 after a stage-by-stage fallback: Process after Flush, the
+ * polyphase_stage.go:300-307 history quirk).  Works on dry-run handles. */
+gar_status gar_stage_state(const gar_resampler *r, int32_t stage, int32_t *fused_plan, int32_t *fused_now);
 
 /* ---- host-only design introspection (no GPU needed) ----------------------- */
 typedef struct gar_engine_geometry {
@@ -217,6 +222,12 @@ gar_status gar_design_engine(double input_rate, double output_rate, int32_t engi
 /* Composite FIR of a fused DFT+polyphase engine: rows [P][taps_max] (zero padded), offsets [P]. */
 gar_status gar_design_composite(double input_rate, double output_rate, int32_t engine_quality, double *rows,
                                 int64_t *offsets);
+
+/* Pipeline stages of a handle (pipeline.BuildPipeline, internal/pipeline/pipeline.go:104-183; 0 when the
+ * ratio is within 0.1 % of 1) and the design geometry + engine ratio of stage `stage`
+ * (engine.NewResampler[float64](48000, 48000*ratio, q), stages.go:54-70). */
+int32_t gar_num_stages(const gar_resampler *r);
+gar_status gar_stage_geometry(const gar_resampler *r, int32_t stage, double *stage_ratio, gar_engine_geometry *geom);
 
 #ifdef __cplusplus
 }

@@ -226,7 +226,37 @@ def test_get_info_fields(gar, O, i, o, preset):
         want = (s0.dft_taps_per_phase * s0.dft_factor if s0.dft_factor > 1 else 0) + \
             s0.poly_taps_per_phase * s0.poly_phases
         assert (inf.FilterLength, inf.Phases) == (want, s0.poly_phases)
-    assert inf.MemoryUsage > 0
+    assert inf.MemoryUsage == _ref_memory_usage(ref, 2)
+
+
+def _ref_memory_usage(ref, channels, max_input_size=0):
+    """MemoryUsage of a fresh reference handle (constant.go:457-468): per channel, the ring
+    buffers' float64 capacity (8192, buffer 0 = MaxInputSize*2 when set: constant.go:72-78) plus
+    StageAdapter.GetMemoryUsage (stage_adapter.go:66-96) -- DFT coefficients factor*taps + history
+    cap 2*taps (dft_stage.go:142), polyphase bank `a` L*taps + history cap 2*taps
+    (polyphase_stage.go:167), float64 elements; decimators and (Quick) cubic stages 64 B
+    (cubicMemoryUsage)."""
+    kinds, _ = ref.stages()
+    per = sum((max_input_size * 2 if (j == 0 and max_input_size > 0) else 8192) * 8 for j in range(len(kinds) + 1))
+    for j in range(len(kinds)):
+        s = ref.stage_info(j)
+        if s.kind == 0:
+            per += 64
+            continue
+        if s.dft_factor > 1:
+            per += (s.dft_factor * s.dft_taps_per_phase + 2 * s.dft_taps_per_phase) * 8
+        if s.poly_phases > 0:
+            per += (s.poly_phases * s.poly_taps_per_phase + 2 * s.poly_taps_per_phase) * 8
+    return per * channels
+
+
+def test_memory_usage_pinned(gar, O):
+    """Hand-derived from the reference code for 44.1k->48k QualityHigh (Quality24Bit: DFT 2 x 200,
+    polyphase 80 x 100) on 2 channels: buffers 2 x 8192 x 8, DFT 2*200*8 + 400*8, poly 80*100*8 + 200*8."""
+    g = gar.New(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True))
+    assert g.GetInfo().MemoryUsage == 2 * (2 * 8192 * 8 + 3200 + 3200 + 64000 + 1600)
+    g = gar.New(gar.Config(44100, 48000, 1, gar.QualityHigh, MaxInputSize=4096, DryRun=True))
+    assert g.GetInfo().MemoryUsage == (4096 * 2 * 8 + 8192 * 8 + 3200 + 3200 + 64000 + 1600)
 
 
 def test_device_api_sample_types(gar):
@@ -256,3 +286,49 @@ def test_pcm_constants_match_header(gar):
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "gar.h")).read()
     m = re.search(r"GAR_PCM16 = (\d+), GAR_PCM24 = (\d+), GAR_PCM32 = (\d+)", hdr)
     assert m and tuple(int(v) for v in m.groups()) == (gar.PCM16, gar.PCM24, gar.PCM32)
+
+
+@pytest.mark.parametrize("dtype", ["F64", "F32"])
+@pytest.mark.parametrize("i,o,chunk", [(96000, 44100, 4800), (48000, 44100, 4096), (44100, 48000, 4096),
+                                       (96000, 16000, 4800)])
+def test_fused_stage_stays_fused_streaming(gar, dtype, i, o, chunk):
+    """A DftPoly stage whose step has no fraction runs on its composite FIR plan (f64 and f32
+    compute) and stays fused through ProcessMulti streaming of 4800/4096-frame chunks -- cfg5's
+    48k->44.1k Quality32Bit stage included (a Pc=294 f64 plan did not fit; buildBgPlan now falls
+    back to Pc=147).  Only Process after Flush switches it to stage-by-stage."""
+    r = gar.New(gar.Config(i, o, 8, gar.QualityVeryHigh, ComputeDtype=getattr(gar, dtype), DryRun=True))
+    nst = r.num_stages()
+    assert nst >= 1
+    fused_stages = [s for s in range(nst) if r.stage_state(s)[0]]
+    assert fused_stages, "no fused stage"
+    xs = [np.zeros(chunk) for _ in range(8)]
+    for _ in range(25):
+        r.ProcessMulti(xs)
+        for s in fused_stages:
+            assert r.stage_state(s) == (True, True)
+    r.FlushMulti()
+    r.ProcessMulti(xs)
+    assert all(r.stage_state(s) == (True, False) for s in fused_stages)
+    r.Reset()
+    assert all(r.stage_state(s) == (True, True) for s in fused_stages)
+
+
+@pytest.mark.parametrize("i,o,preset", [(96000, 44100, 4), (44100, 48000, 3), (96000, 16000, 3), (48000, 44100, 4)])
+def test_stage_geometry_matches_oracle_pipeline(gar, O, i, o, preset):
+    """gar_num_stages / gar_stage_geometry report the pipeline of pipeline.BuildPipeline
+    (pipeline.go:104-183) and each stage's engine design, as the oracle builds them."""
+    r = gar.New(gar.Config(i, o, 2, preset, DryRun=True))
+    ref = O.NewResampler(i, o, 1, preset)
+    kinds, ratios = ref.stages()
+    assert r.num_stages() == len(kinds)
+    for j in range(len(kinds)):
+        ratio, g = r.stage_geometry(j)
+        assert ratio == pytest.approx(ratios[j], rel=1e-15)
+        s = ref.stage_info(j)
+        assert g.kind == s.kind
+        if s.dft_factor > 1:
+            assert (g.dft_factor, g.dft_taps) == (s.dft_factor, s.dft_taps_per_phase)
+        if s.poly_phases:
+            assert (g.poly_phases, g.poly_taps, g.poly_step) == (s.poly_phases, s.poly_taps_per_phase, s.poly_step)
+        if s.decim_factor:
+            assert (g.decim_factor, g.decim_taps) == (s.decim_factor, s.decim_taps)

@@ -99,3 +99,42 @@ def test_gloo_two_ranks_resample_shards(O):
     assert (n0, n1) == (32, 32)
     assert out0 == out1 == 32 * 2 * per_channel
     assert t0 == t1 == 64 * 2 * per_channel
+
+
+def _run_bench(nproc, extra):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    args = ["--dry-run", "--steps", "2", "--warmup", "1"] + extra
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(root, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py")] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 prints one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_main_two_ranks_dry_run():
+    """bench.py main() end to end under torch.distributed.run with WORLD_SIZE=2 (gloo, dry-run
+    handles = the exact host state machine): cfg4's 1024 streams sharded one NewBatch per
+    rank, the counters reduced over ranks, equal the single-rank totals; the weak-scaled
+    secondary (cfg5 per rank) doubles."""
+    extra = ["--workload", "cfg4", "--seconds", "0.5", "--secondary", "cfg5"]
+    one = _run_bench(1, extra)
+    two = _run_bench(2, extra)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["dry_run"] is True
+    assert two["input_samples_total"] == one["input_samples_total"] == 1024 * 2 * 22050
+    assert two["output_samples_total"] == one["output_samples_total"]
+    assert two["config"]["streams_per_gpu"] == 512 and one["config"]["streams_per_gpu"] == 1024
+    s1, s2 = one["secondary"]["cfg5"], two["secondary"]["cfg5"]
+    assert s2["input_samples_total"] == 2 * s1["input_samples_total"]
+    assert s2["output_samples_total"] == 2 * s1["output_samples_total"]

@@ -154,3 +154,25 @@ def test_hx_zero_input(gar, O, cuda):
     x = np.zeros((20000, 2))
     got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
     assert np.all(got == 0.0)
+
+
+def test_hx_loud_many_columns(gar, O, cuda):
+    """Loud samples (|x| >= 16) in several columns of one 16-column block and in many blocks of
+    one launch (16 channels: ROW16 loads, every block holds loud columns): each output whose
+    window holds one is recomputed exactly after the block (hxsFixup), for every column."""
+    n, ch = 120000, 16
+    x = signal(n, ch, 48000, seed=21).astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(5)
+    for c in range(ch):
+        for t in rng.integers(0, n, size=6):
+            x[t, c] = (1 if rng.random() < 0.5 else -1) * 10.0 ** rng.uniform(1.3, 5)
+    x = x.astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 48000, 44100, x, gar.QualityVeryHigh, gar.F32)
+    want = oracle_new(O, 48000, 44100, x, O.P_VERYHIGH)
+    ex = run(gar, cuda, 48000, 44100, x, gar.QualityVeryHigh, gar.F32_EXACT)
+    for c in range(ch):
+        assert got.shape[0] == len(want[c])
+        assert rms(got[:, c], want[c]) <= max(3.0 * rms(ex[:, c], want[c]), F32_RMS_TOL)
+        big = np.abs(np.asarray(want[c])) > 20
+        assert big.any()
+        assert np.max(np.abs(got[big, c] - want[c][big]) / np.abs(want[c][big])) <= 1e-6
