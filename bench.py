@@ -268,8 +268,10 @@ def pmc_traffic(args, workload, kernel_keys):
                     grid[key] = int(float(row.get("Grid_Size") or 0))
         if not per:
             return None, f"{counter}: no dispatch of {kernel_keys}"
-        gmax = max(grid.values())
-        vals = [v for k, v in per.items() if grid[k] == gmax]
+        # the stream-body launch moves the most bytes (a flush tail or a batch's small launches can
+        # have the larger grid): average the dispatches within 1 % of the largest count
+        vmax = max(per.values())
+        vals = [v for v in per.values() if v >= 0.99 * vmax]
         out[counter] = sum(vals) / len(vals)
     corr = FETCH_CORRECTION[LOAD_WIDTH.get(workload, 16)]
     rd = out["FETCH_SIZE"] * 1024 * corr
@@ -284,8 +286,10 @@ KIND_NAMES = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR",
               4: "polyphase with live cubic coefficients (poly_kernel)", 5: "QualityQuick cubic stage (cubic_kernel)"}
 # profile kind -> engine kind of the stage it runs (gar_engine_geometry.kind: 1 DFT-only, 2 DFT+poly, 3 decim, 0 cubic)
 KIND_STAGE = {0: (2,), 1: (1, 2), 2: (3,), 4: (2,), 5: (0,)}
-# gfx950 FETCH_SIZE under-count per load width (MI355X_MICROARCH.md HBM section: x2 for 16-B/lane
-# streaming reads; other widths calibrated on a known byte count, profiles/r03_fetch_calib.txt)
+# gfx950 FETCH_SIZE under-count per load width: MI355X_MICROARCH.md's HBM section gives x2 for
+# 16-B/lane streaming reads; calibrated here on 1 GiB read once with buffer_load_dwordx4/x2/dword
+# (tools/ubench/fetch_calib.hip, profiles/r03_fetch_calib.txt): FETCH_SIZE = 0.500 of the bytes at
+# 16, 8 and 4 B/lane; WRITE_SIZE = 1.000 at 16 and 8 B/lane
 FETCH_CORRECTION = {16: 2.0, 8: 2.0, 4: 2.0}
 
 

@@ -166,3 +166,123 @@ def precision_thd(y, freq, rate):
     fm = abs(X[fb])
     hp = sum(abs(X[fb * h]) ** 2 for h in range(2, 6) if fb * h < F // 2)
     return 10 * np.log10(hp / fm ** 2)
+
+
+# ----------------------------------------------------------------------------- anti-aliasing / impulse
+# internal/engine/antialiasing_test.go:21-27, quality_comparison_test.go:578-648
+ANTIALIAS_SAMPLES = 32768
+FFT_WINDOW = 8192
+MIN_STOPBAND_ATT = 80.0
+NOISE, MULTITONE, SWEEP, ALIAS_TONES = "noise", "multitone", "sweep", "alias_tones"
+
+
+def antialias_signal(kind, rate, n=ANTIALIAS_SAMPLES):
+    """generateAntialiasTestSignal (antialiasing_test.go:56-117)."""
+    x = np.zeros(n)
+    i = np.arange(n)
+    if kind == NOISE:  # LCG, uint32 state
+        st = 12345
+        v = np.empty(n)
+        for k in range(n):
+            st = (st * 1103515245 + 12345) & 0xFFFFFFFF
+            v[k] = float(st & 0x7FFFFFFF) / float(0x7FFFFFFF) * 2.0 - 1.0
+        x = v * 0.5
+    elif kind == MULTITONE:
+        for f in (1000, 2000, 4000, 8000, 12000, 16000, 20000, 22000, 23000):
+            if f < rate / 2.0 * 0.95:
+                x += 0.1 * np.sin(2.0 * np.pi * f * i / rate)
+    elif kind == SWEEP:
+        f0, f1 = 100.0, rate * 0.45
+        rate_s = (f1 - f0) / (n / rate)
+        t = i / rate
+        x = 0.7 * np.sin(2.0 * np.pi * (f0 * t + rate_s * t * t / 2.0))
+    elif kind == ALIAS_TONES:  # 48->32 estimate of the output Nyquist (sampleRate / 3)
+        f = rate / 3.0 + 1000
+        while f < rate / 2.0 - 500:
+            x += 0.1 * np.sin(2.0 * np.pi * f * i / rate)
+            f += 1000
+    return x
+
+
+def alias_tones(in_rate, out_rate, n=ANTIALIAS_SAMPLES):
+    """generateAliasTones (antialiasing_test.go:617-633): 0.1-amplitude tones from the output
+    Nyquist + 1 kHz to the input Nyquist - 500 Hz, 1 kHz apart."""
+    x = np.zeros(n)
+    i = np.arange(n)
+    f = out_rate / 2.0 + 1000
+    while f < in_rate / 2.0 - 500:
+        x += 0.1 * np.sin(2.0 * np.pi * f * i / in_rate)
+        f += 1000
+    return x
+
+
+def compute_psd(sig, rate, fft_size=FFT_WINDOW):
+    """computePSD (antialiasing_test.go:123-177): Welch, Hann (N-1), 50 % overlap, dB."""
+    sig = np.asarray(sig, dtype=np.float64)
+    nb = fft_size // 2 + 1
+    freqs = np.arange(nb) * rate / fft_size
+    w = 0.5 * (1.0 - np.cos(2.0 * np.pi * np.arange(fft_size) / (fft_size - 1)))
+    acc = np.zeros(nb)
+    nwin = 0
+    for s in range(0, len(sig) - fft_size + 1, fft_size // 2):
+        X = go_fft(sig[s:s + fft_size] * w)
+        acc += np.abs(X[:nb]) ** 2
+        nwin += 1
+    power = acc / (nwin * fft_size * float(np.sum(w * w)))
+    with np.errstate(divide="ignore"):
+        psd = np.where(power > 1e-20, 10.0 * np.log10(np.maximum(power, 1e-300)), -200.0)
+    return freqs, psd
+
+
+def band_energy(freqs, psd, lo, hi):
+    """measureBandEnergy (antialiasing_test.go:232-248)."""
+    sel = (freqs >= lo) & (freqs < hi)
+    if not sel.any():
+        return -200.0
+    return float(10.0 * np.log10(np.sum(10.0 ** (psd[sel] / 10.0)) / sel.sum()))
+
+
+def peak_energy(freqs, psd, lo, hi):
+    """measurePeakEnergy (antialiasing_test.go:250-262)."""
+    sel = (freqs >= lo) & (freqs < hi)
+    return float(max(-200.0, psd[sel].max())) if sel.any() else -200.0
+
+
+def antialiasing(run, in_rate, out_rate, kind):
+    """measureAntiAliasing (antialiasing_test.go:276-348): stopband (imaging region above the
+    input Nyquist) attenuation of an upsampler; peak-based for multitone, average otherwise."""
+    y = run(antialias_signal(kind, in_rate))
+    f, p = compute_psd(y, out_rate)
+    pb_end = in_rate / 2.0 * 0.9
+    sb0, sb1 = in_rate / 2.0 + 1000, out_rate / 2.0 - 1000
+    meas = peak_energy if kind == MULTITONE else band_energy
+    return meas(f, p, 100, pb_end) - meas(f, p, sb0, sb1)
+
+
+def downsampling_antialiasing(run, in_rate, out_rate):
+    """measureDownsamplingAntiAliasing (antialiasing_test.go:635-699): alias tones' input
+    peak minus the output's peak where they would fold ([out - in/2, out/2])."""
+    x = alias_tones(in_rate, out_rate)
+    y = run(x)
+    fi, pi_ = compute_psd(x, in_rate)
+    fo, po = compute_psd(y, out_rate)
+    inp = peak_energy(fi, pi_, out_rate / 2.0 + 500, in_rate / 2.0 - 500)
+    lo = max(out_rate - in_rate / 2.0, 100.0)
+    return inp - peak_energy(fo, po, lo, out_rate / 2.0)
+
+
+def impulse_response(run, n=8192):
+    """measureImpulseResponse (quality_comparison_test.go:578-648): unit impulse at n/2;
+    pre-ringing peak before the main peak, post-ringing peak from 10 samples after it (dB
+    re the main peak), ring-out = last sample above -60 dB."""
+    x = np.zeros(n)
+    x[n // 2] = 1.0
+    y = np.abs(np.asarray(run(x), dtype=np.float64))
+    k = int(np.argmax(y))  # first maximum, as the Go loop's strict '>'
+    m = y[k]
+    pre = y[:k].max() if k > 0 else 0.0
+    post = y[k + 10:].max() if k + 10 < len(y) else 0.0
+    above = np.nonzero(y[k:] > m * 10 ** (-60.0 / 20.0))[0]
+    return {"pre_ringing_db": float(20 * np.log10(pre / m + 1e-20)),
+            "post_ringing_db": float(20 * np.log10(post / m + 1e-20)),
+            "ringout_samples": int(above[-1]) if len(above) else 0, "peak_index": k}
