@@ -11,11 +11,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gar.h"
@@ -390,6 +395,125 @@ struct PinBuf {
     }
 };
 
+// Pinned host buffer the kernels read / write in place (the host C-ABI's staging: the caller's
+// pageable arrays are packed into it on the host, the first stage's kernel reads it over PCIe and
+// the last stage's kernel writes its outputs into the output one -- no DMA round trip per call).
+// Used only between a launch and the stream synchronise of the same call.
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    unsigned flags = 0;
+    HostBuf() = default;
+    explicit HostBuf(unsigned f) : flags(f) {}
+    HostBuf(const HostBuf&) = delete;
+    HostBuf& operator=(const HostBuf&) = delete;
+    ~HostBuf() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    void* ensure(size_t bytes) {
+        if (bytes <= cap) return p;
+        release();
+        const size_t nb = bytes + bytes / 4 + 4096;
+        HIPCHK(hipHostMalloc(&p, nb, hipHostMallocMapped | flags));
+        cap = nb;
+        return p;
+    }
+};
+
+// Host worker pool for packing / unpacking large host C-ABI calls (one job split over
+// min(15, cores - 1) workers + the caller); small calls run inline.
+class Pool {
+   public:
+    static Pool& get() {
+        static Pool p;
+        return p;
+    }
+    void run(int n, const std::function<void(int)>& f) {
+        if (n <= 1 || th_.empty()) {
+            for (int i = 0; i < n; ++i) f(i);
+            return;
+        }
+        std::unique_lock<std::mutex> lk(mu_);
+        job_ = &f;
+        njobs_ = n;
+        next_.store(0);
+        pending_ = n;
+        ++gen_;
+        cv_.notify_all();
+        lk.unlock();
+        work();
+        lk.lock();
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    int workers() const { return static_cast<int>(th_.size()) + 1; }
+
+   private:
+    Pool() {
+        const unsigned hw = std::thread::hardware_concurrency();
+        const int n = std::max(0, std::min<int>(15, static_cast<int>(hw) - 1));
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void work() {
+        for (;;) {
+            const int i = next_.fetch_add(1);
+            if (i >= njobs_) return;
+            (*job_)(i);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
+            if (stop_) return;
+            seen = gen_;
+            lk.unlock();
+            work();
+            lk.lock();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int njobs_ = 0, pending_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Runs f(c, lo, hi) over channels x [0, n) samples: inline below ~1 MiB of data, else split
+// into slices over the pool.
+inline void forSlices(int C, int64_t n, size_t bytesPerSample, const std::function<void(int, int64_t, int64_t)>& f) {
+    const size_t total = static_cast<size_t>(C) * static_cast<size_t>(std::max<int64_t>(n, 0)) * bytesPerSample;
+    if (total < (size_t(1) << 20)) {
+        for (int c = 0; c < C; ++c) f(c, 0, n);
+        return;
+    }
+    Pool& pool = Pool::get();
+    const int per = std::max<int>(1, (pool.workers() * 2 + C - 1) / C);  // slices per channel
+    const int64_t step = (n + per - 1) / per;
+    pool.run(C * per, [&](int i) {
+        const int c = i / per, k = i - c * per;
+        const int64_t lo = k * step, hi = std::min<int64_t>(n, lo + step);
+        if (lo < hi) f(c, lo, hi);
+    });
+}
+
 struct Group {
     int c0 = 0, C = 1;
     std::vector<Counters> cnt;
@@ -427,6 +551,8 @@ struct gar_resampler {
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
     gar::DevBuf inStage, outStage;
+    // host C-ABI staging: pinned, mapped; input write-combined (the host only writes it)
+    gar::HostBuf hostIn{hipHostMallocWriteCombined | hipHostMallocCoherent}, hostOut{hipHostMallocCoherent};
     std::vector<int64_t> scratchSizes;
     // optional HIP-event timing of the MFMA FIR launches (bench.py roofline)
     bool profile = false;
@@ -954,16 +1080,20 @@ gar_status wrap(F&& f) {
 // the handle's previous call (any stream), recorded for the next; a device
 // error poisons the handle until Reset.
 template <class F>
-gar_status callOn(Handle* h, hipStream_t s, F&& f) {
+gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
     if (h->poisoned) return guard(GAR_ERR_DEVICE, "handle unusable after an earlier device error; call Reset");
     if (h->dry) return wrap(f);
     DeviceGuard dg(h->device);
     const gar_status st = wrap([&]() -> gar_status {
         if (h->orderValid && h->lastStream != s) HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
         const gar_status r = f();
-        HIPCHK(hipEventRecord(h->orderEv, s));
-        h->lastStream = s;
-        h->orderValid = true;
+        if (hostSynced) {  // the call synchronised its stream: nothing of it is left to order after
+            h->orderValid = false;
+        } else {
+            HIPCHK(hipEventRecord(h->orderEv, s));
+            h->lastStream = s;
+            h->orderValid = true;
+        }
         return r;
     });
     if (st == GAR_ERR_DEVICE) h->poisoned = true;
@@ -1113,19 +1243,27 @@ int64_t estimate(const Handle* h, int64_t n) {
     return static_cast<int64_t>(static_cast<double>(n) * h->ratio) + 64;
 }
 
-// H2D a host vector into the input staging buffer.
-InView stageIn(Handle* h, const void* in, int64_t n, int f64) {
-    InView v;
-    v.n = n;
-    v.f64 = f64;
-    v.fs = 1;
-    v.cs = 0;
-    if (h->dry || n == 0) return v;
-    const size_t es = f64 ? 8 : 4;
-    h->inStage.ensure(n * es);
-    HIPCHK(hipMemcpyAsync(h->inStage.p, in, n * es, hipMemcpyHostToDevice, h->stream));
-    v.p = h->inStage.p;
-    return v;
+// Host input -> pinned staging in the compute dtype (f64 -> f32 rounds exactly as the kernels'
+// loads would: the result is bit-identical to handing them the f64 input).
+template <class T>
+void packChannel(void* dst, bool f64, const T* src, int64_t lo, int64_t hi) {
+    if (f64) {
+        double* d = static_cast<double*>(dst);
+        for (int64_t i = lo; i < hi; ++i) d[i] = static_cast<double>(src[i]);
+    } else {
+        float* d = static_cast<float*>(dst);
+        for (int64_t i = lo; i < hi; ++i) d[i] = static_cast<float>(src[i]);
+    }
+}
+template <class T>
+void unpackChannel(T* dst, bool f64, const void* src, int64_t lo, int64_t hi) {
+    if (f64) {
+        const double* s = static_cast<const double*>(src);
+        for (int64_t i = lo; i < hi; ++i) dst[i] = static_cast<T>(s[i]);
+    } else {
+        const float* s = static_cast<const float*>(src);
+        for (int64_t i = lo; i < hi; ++i) dst[i] = static_cast<T>(s[i]);
+    }
 }
 
 template <class T>
@@ -1136,7 +1274,7 @@ gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t c
     if (nOut) *nOut = 0;
     if (!flush && n < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
     if (!flush && intoSemantics && cap < estimate(h, n)) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
-    const int f64 = sizeof(T) == 8 ? 1 : 0;
+    const size_t es = h->f64 ? 8 : 4;  // compute dtype: the staging holds exactly what the kernels compute in
     return callOn(h, h->stream, [&]() -> gar_status {
         isolate(h, ch);
         Group* g = groupOf(h, ch);
@@ -1146,23 +1284,33 @@ gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t c
             if (intoSemantics && !flush) { g_err = "EstimateOutput underestimated actual output length"; return GAR_ERR_INTERNAL; }
             return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
         }
-        const InView iv = flush ? InView() : stageIn(h, in, n, f64);
+        InView iv;
+        iv.n = flush ? 0 : n;
+        iv.f64 = h->f64 ? 1 : 0;
+        iv.fs = 1;
+        iv.cs = 0;
         OutView ov;
         ov.fs = 1;
         ov.cs = 0;
-        ov.f64 = f64;
+        ov.f64 = h->f64 ? 1 : 0;
         if (!h->dry) {
-            h->outStage.ensure(std::max<int64_t>(need, 1) * sizeof(T));
-            ov.p = h->outStage.p;
+            if (!flush && n > 0) {
+                void* hp = h->hostIn.ensure(static_cast<size_t>(n) * es);
+                forSlices(1, n, es + sizeof(T), [&](int, int64_t lo, int64_t hi) { packChannel<T>(hp, h->f64, in, lo, hi); });
+                iv.p = hp;
+            }
+            ov.p = h->hostOut.ensure(static_cast<size_t>(std::max<int64_t>(need, 1)) * es);
         }
         gar_status st;
         const int64_t got = runGroup(h, *g, iv, ov, flush, h->stream, cap, st);
         if (st != GAR_OK) return st;
-        if (!h->dry && got > 0) HIPCHK(hipMemcpyAsync(out, h->outStage.p, got * sizeof(T), hipMemcpyDeviceToHost, h->stream));
-        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        if (!h->dry) {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            forSlices(1, got, es + sizeof(T), [&](int, int64_t lo, int64_t hi) { unpackChannel<T>(out, h->f64, ov.p, lo, hi); });
+        }
         if (nOut) *nOut = got;
         return GAR_OK;
-    });
+    }, true);
 }
 
 }  // namespace
@@ -1319,6 +1467,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
         g_err = "expected " + std::to_string(r->channels) + " channels, got " + std::to_string(nch);
         return GAR_ERR_CHANNEL_MISMATCH;
     }
+    if (n < 0) return guard(GAR_ERR_INVALID_ARGUMENT, "negative length");
     return callOn(r, r->stream, [&]() -> gar_status {
         gar_resampler* h = r;
         // exact sizes first: no state changes on BUFFER_TOO_SMALL
@@ -1327,40 +1476,50 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
             if (simulate(h, g, n, false, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
         }
         const int C = h->channels;
-        InView base;
-        base.n = n;
-        base.f64 = 1;
-        base.fs = 1;
-        base.cs = n;
-        if (!h->dry && n > 0) {
-            h->inStage.ensure(static_cast<size_t>(n) * C * 8);
-            for (int c = 0; c < C; ++c)
-                HIPCHK(hipMemcpyAsync(static_cast<char*>(h->inStage.p) + static_cast<size_t>(c) * n * 8, in[c], n * 8,
-                                      hipMemcpyHostToDevice, h->stream));
+        const size_t es = h->f64 ? 8 : 4;
+        // planar [channel][frame] in the compute dtype; output rows 16-B aligned (vector stores)
+        const int64_t ocap = (std::max<int64_t>(cap, 1) + 3) / 4 * 4;
+        char* hin = nullptr;
+        char* hout = nullptr;
+        if (!h->dry) {
+            if (n > 0) {
+                hin = static_cast<char*>(h->hostIn.ensure(static_cast<size_t>(n) * C * es));
+                forSlices(C, n, es + 8, [&](int c, int64_t lo, int64_t hi) {
+                    packChannel<double>(hin + static_cast<size_t>(c) * n * es, h->f64, in[c], lo, hi);
+                });
+            }
+            hout = static_cast<char*>(h->hostOut.ensure(static_cast<size_t>(ocap) * C * es));
         }
-        const int64_t ocap = std::max<int64_t>(cap, 1);
-        if (!h->dry) h->outStage.ensure(static_cast<size_t>(ocap) * C * 8);
-        for (auto& g : h->groups) {
-            InView iv = base;
-            if (!h->dry) iv.p = static_cast<const char*>(h->inStage.p) + static_cast<size_t>(g.c0) * n * 8;
+        std::vector<int64_t> got(h->groups.size());
+        for (size_t gi = 0; gi < h->groups.size(); ++gi) {
+            Group& g = h->groups[gi];
+            InView iv;
+            iv.n = n;
+            iv.f64 = h->f64 ? 1 : 0;
+            iv.fs = 1;
+            iv.cs = n;
+            if (hin) iv.p = hin + static_cast<size_t>(g.c0) * n * es;
             OutView ov;
-            ov.f64 = 1;
+            ov.f64 = h->f64 ? 1 : 0;
             ov.fs = 1;
             ov.cs = ocap;
-            if (!h->dry) ov.p = static_cast<char*>(h->outStage.p) + static_cast<size_t>(g.c0) * ocap * 8;
+            if (hout) ov.p = hout + static_cast<size_t>(g.c0) * ocap * es;
             gar_status st;
-            const int64_t got = runGroup(h, g, iv, ov, false, h->stream, cap, st);
+            got[gi] = runGroup(h, g, iv, ov, false, h->stream, cap, st);
             if (st != GAR_OK) return st;
-            for (int c = g.c0; c < g.c0 + g.C; ++c) {
-                if (n_out) n_out[c] = got;
-                if (!h->dry && got > 0)
-                    HIPCHK(hipMemcpyAsync(out[c], static_cast<char*>(h->outStage.p) + static_cast<size_t>(c) * ocap * 8,
-                                          got * 8, hipMemcpyDeviceToHost, h->stream));
-            }
+            for (int c = g.c0; c < g.c0 + g.C; ++c)
+                if (n_out) n_out[c] = got[gi];
         }
-        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        if (!h->dry) {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            const int64_t gmax = got.empty() ? 0 : *std::max_element(got.begin(), got.end());
+            forSlices(C, gmax, es + 8, [&](int c, int64_t lo, int64_t hi) {
+                const int64_t m = got[groupOf(h, c) - h->groups.data()];
+                if (lo < m) unpackChannel<double>(out[c], h->f64, hout + static_cast<size_t>(c) * ocap * es, lo, std::min(hi, m));
+            });
+        }
         return GAR_OK;
-    });
+    }, true);
 }
 
 gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch, int64_t cap, int64_t* n_out) {
@@ -1373,27 +1532,33 @@ gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch
             if (simulate(h, g, 0, true, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
         }
         const int C = h->channels;
-        const int64_t ocap = std::max<int64_t>(cap, 1);
-        if (!h->dry) h->outStage.ensure(static_cast<size_t>(ocap) * C * 8);
-        for (auto& g : h->groups) {
+        const size_t es = h->f64 ? 8 : 4;
+        const int64_t ocap = (std::max<int64_t>(cap, 1) + 3) / 4 * 4;
+        char* hout = h->dry ? nullptr : static_cast<char*>(h->hostOut.ensure(static_cast<size_t>(ocap) * C * es));
+        std::vector<int64_t> got(h->groups.size());
+        for (size_t gi = 0; gi < h->groups.size(); ++gi) {
+            Group& g = h->groups[gi];
             OutView ov;
-            ov.f64 = 1;
+            ov.f64 = h->f64 ? 1 : 0;
             ov.fs = 1;
             ov.cs = ocap;
-            if (!h->dry) ov.p = static_cast<char*>(h->outStage.p) + static_cast<size_t>(g.c0) * ocap * 8;
+            if (hout) ov.p = hout + static_cast<size_t>(g.c0) * ocap * es;
             gar_status st;
-            const int64_t got = runGroup(h, g, InView(), ov, true, h->stream, cap, st);
+            got[gi] = runGroup(h, g, InView(), ov, true, h->stream, cap, st);
             if (st != GAR_OK) return st;
-            for (int c = g.c0; c < g.c0 + g.C; ++c) {
-                if (n_out) n_out[c] = got;
-                if (!h->dry && got > 0)
-                    HIPCHK(hipMemcpyAsync(out[c], static_cast<char*>(h->outStage.p) + static_cast<size_t>(c) * ocap * 8,
-                                          got * 8, hipMemcpyDeviceToHost, h->stream));
-            }
+            for (int c = g.c0; c < g.c0 + g.C; ++c)
+                if (n_out) n_out[c] = got[gi];
         }
-        if (!h->dry) HIPCHK(hipStreamSynchronize(h->stream));
+        if (!h->dry) {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            const int64_t gmax = got.empty() ? 0 : *std::max_element(got.begin(), got.end());
+            forSlices(C, gmax, es + 8, [&](int c, int64_t lo, int64_t hi) {
+                const int64_t m = got[groupOf(h, c) - h->groups.data()];
+                if (lo < m) unpackChannel<double>(out[c], h->f64, hout + static_cast<size_t>(c) * ocap * es, lo, std::min(hi, m));
+            });
+        }
         return GAR_OK;
-    });
+    }, true);
 }
 
 int64_t gar_device_output_size(const gar_resampler* r, int64_t frames) {

@@ -74,6 +74,7 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
         case 0: return hxsLaunch<NS, 0>(x, lds, blocks, st);
         case 1: return hxsLaunch<NS, 1>(x, lds, blocks, st);
         case 2: return hxsLaunch<NS, 2>(x, lds, blocks, st);
+        case 4: return hxsLaunch<NS, 4>(x, lds, blocks, st);
         default: return hxsLaunch<NS, 3>(x, lds, blocks, st);
     }
 }
@@ -209,7 +210,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.out_fs = od.fs * esz;
     x.out_cs = od.cs * esz;
     const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
-    if (od.pcm == 16 && al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;  // int16 stereo frame pairs
+    if (od.pcm == 16 && al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 4;  // int16 stereo frame pairs
     else if (od.pcm) x.vst = 0;  // other PCM stores: the epilogue's checked per-element path
     else if (od.f64) x.vst = 3;
     else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;

@@ -46,6 +46,15 @@ constexpr int kHxsD = GAR_HXS_D;                        // loads in flight per l
 constexpr int kHxsNP = GAR_HXS_NP;                      // 64-row pieces per load (G*Qc <= 768: cfg2 G = 5)
 constexpr int kHxsMaxG = 6;                             // periods per group (launcher: largest that fits)
 constexpr int kHxsItems = (4 * kHxsNP + kHxsLoaders - 1) / kHxsLoaders;  // (quad, piece) items per loader per load
+// Development instrumentation (GAR_HXS_DBG attribution modes, GAR_HXS_PROF phase cycles): compiled
+// in only with -DGAR_HXS_DEV=1 (tools/hxs_variant.sh); the production kernel carries none of it.
+#ifndef GAR_HXS_DEV
+#define GAR_HXS_DEV 0
+#endif
+constexpr bool kHxsDev = GAR_HXS_DEV != 0;
+#ifndef GAR_HXS_PF2
+#define GAR_HXS_PF2 0  // B fragments two steps ahead (A/B builds)
+#endif
 
 struct HxsArgs {
     const h8v* A;          // [nprog][NS][2][64] f16x8
@@ -392,9 +401,14 @@ __device__ __forceinline__ int32_t pcm16Of(float y) {
     return v == v ? static_cast<int32_t>(v) : 0;
 }
 
+// Interior store of a lane's four rows.  VST (the launch's output layout, a template parameter so
+// the epilogue carries no layout branches): 0 any f32 layout (4 stores), 1 channel-contiguous f32
+// (one 16-B store), 2 stereo-interleaved f32 (lane pairs swap halves by DPP: one 16-B store of two
+// frames each), 3 f64 (4 stores), 4 stereo-interleaved PCM16 (two int16 frames, 8 B).
 template <int VST>
 __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y, int lane) {
-    if (VST == 2) {
+    const bool nt = kHxsDev && x.nt;
+    if (VST == 2 || VST == 4) {
         const bool even = (lane & 1) == 0;
         const float s0 = even ? y[2] : y[0], s1 = even ? y[3] : y[1];
         const float q0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xf, 0xf, false));
@@ -402,26 +416,23 @@ __device__ __forceinline__ void hxsStoreFast(const HxsArgs& x, char* p, f32x4 y,
         f32x4 w;
         if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
         else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
-        if (x.out_pcm == 16) {  // two int16 stereo frames (8 B): clamp, x32767, truncate (main.go:497-541)
+        if constexpr (VST == 4) {  // two int16 stereo frames (8 B): clamp, x32767, truncate (main.go:497-541)
             const int32_t i0 = pcm16Of(w[0]), i1 = pcm16Of(w[1]), i2 = pcm16Of(w[2]), i3 = pcm16Of(w[3]);
             uint2 v;
             v.x = (static_cast<uint32_t>(i0) & 0xffffu) | (static_cast<uint32_t>(i1) << 16);
             v.y = (static_cast<uint32_t>(i2) & 0xffffu) | (static_cast<uint32_t>(i3) << 16);
             *reinterpret_cast<uint2*>(p) = v;
-        } else if (x.nt) {
+        } else if (nt) {
             __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
         } else {
             *reinterpret_cast<f32x4*>(p) = w;
         }
     } else if (VST == 1) {
-        if (x.nt) __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(p));
+        if (nt) __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(p));
         else *reinterpret_cast<f32x4*>(p) = y;
     } else if (VST == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (x.nt) __builtin_nontemporal_store(y[i], reinterpret_cast<float*>(p + i * x.out_fs));
-            else *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
-        }
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<float*>(p + i * x.out_fs) = y[i];
     } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) *reinterpret_cast<double*>(p + i * x.out_fs) = static_cast<double>(y[i]);
@@ -505,49 +516,31 @@ __device__ __forceinline__ void hxsRegConvert(XP x, const HxsStage& st, bool fas
 }
 
 // Compute waves (one row block each).
-template <int NS, int VST>
-__device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh_, int wt, int lane) {
-    const uint32_t QS = sh_.QS;
+// Per block a wave decides once whether every period of its 16 columns is an interior, fully
+// stored row block ("fast": the common case -- all but the launch's edge blocks); then the
+// epilogue of a period is scale + (stereo) lane swap + one 16-B store at a pointer advanced by a
+// constant per period, with no per-period range checks or 64-bit index arithmetic.
+template <int NS, int VST, bool FAST>
+__device__ __forceinline__ void hxsGroups(const HxsArgs& x, const HxsShared& sh_, int lane, const h8v (&Ah)[NS],
+                                          const h8v (&Al)[NS], uint32_t laneOff, int u0, int P, int nslot,
+                                          char* obase, int64_t pstride, int64_t aCol, int64_t oRow0, bool colOk,
+                                          int ccol, bool fullRb, unsigned long long& tm, unsigned long long& tw) {
     const int sh = -(x.ea + kHxXs);
     const int GQ = x.G * x.Qc;
-    const int grp = lane >> 4, l16 = lane & 15;
-    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
-    const int* pt = x.progs + kBgProgInts * wt;
-    const int u0 = uni(pt[4]), rbw = uni(pt[3]);
-    const int tid = wt * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
-    h8v Ah[NS], Al[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-        Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
-        Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
-    }
-    const bool fullRb = (rbw + 1) * 16 <= x.Pc;
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
     const uint32_t pstep = 8u * static_cast<uint32_t>(x.Qc);
-    const int nslot = x.R / GQ;
-    unsigned long long tm = 0, tw = 0, tcv = 0;
-
-    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ, nL = x.small ? 0 : P + x.ngroups - 1;
-
-    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
-        const int b = hxsBlock(x, bi);
-        hxsBarrier();  // loud state reset; the previous block's ring reads done
-        if (x.small) hxsSmallStage(&x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
-        hxsBarrier();  // load 0 landed (small: the whole window in the ring)
-        const int col = b * 16 + l16;
-        const bool colOk = col < x.ncols;
-        const int kcol = col / x.C, ccol = col - kcol * x.C;
-        const int64_t aCol = x.a_lo + static_cast<int64_t>(kcol) * x.Np;
-        const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;  // first row of this lane's accumulator
-        // output of relative period p: whole-quad store, or checked elements at the launch edges
-        auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
-            const f32x4 y = hxScale(oA, oL, sh);
+    const int dbg = kHxsDev ? x.dbg : 0;
+    auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
+        const f32x4 y = hxScale(oA, oL, sh);
+        if (dbg & 2) return;
+        if constexpr (FAST) {
+            hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride, y, lane);
+        } else {
             const int64_t a = aCol + p;
             const int64_t o0 = a * x.Pc + oRow0;
             const bool live = colOk && p < x.Np && a < x.a_hi;
-            if (x.dbg & 2) {
-            } else if (fullRb && live && (!x.out_pcm || VST == 2) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
-                char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
+            if (fullRb && live && (!x.out_pcm || VST == 4) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+                char* pp = x.out + (o0 + (((VST == 2 || VST == 4) && (lane & 1)) ? 2 : 0)) * x.out_fs + ((VST == 2 || VST == 4) ? 0 : ccol * x.out_cs);
                 hxsStoreFast<VST>(x, pp, y, lane);
             } else if (live) {
 #pragma unroll
@@ -561,54 +554,62 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
                     }
                 }
             }
-        };
-        const int nstepsPad = hxsStepsPad(x);
-        for (int j = 0; j < nstepsPad; ++j) {
-            // load j -> ring (this wave's share), then the MFMA periods of group j - P
-            const unsigned long long t0 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            if (x.prof) tcv += __builtin_amdgcn_s_memtime() - t0;
-            const int g = j - P;
-            if (g < 0 || g >= x.ngroups) {
-                hxsBarrier();
-                continue;
-            }
-            const int slot = g % nslot;
-            uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(sh_.ring + laneOff))) +
-                          8u * static_cast<uint32_t>(slot * GQ + u0);
-            h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
-            // one period's MFMA program into nA (hi-x products) and nL (lo-x products); the
-            // epilogue of period ep (oA, oL) issues after its first step when epi
-            auto period = [&](f32x4& nA, f32x4& nL, const f32x4& oA, const f32x4& oL, bool epi, int ep, bool last) {
-                asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
-                const uint32_t aL = aH + dL, aN = aH + pstep, aNL = aN + dL;
-                nA = f32x4{0, 0, 0, 0};
-                nL = nA;
+        }
+    };
+    const int nstepsPad = hxsStepsPad(x);
+    for (int j = 0; j < nstepsPad; ++j) {
+        // load j -> ring (the loaders' share), then the MFMA periods of group j - P
+        const unsigned long long t0 = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+        const int g = j - P;
+        if (g < 0 || g >= x.ngroups) {
+            hxsBarrier();
+            continue;
+        }
+        const int slot = g % nslot;
+        uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(sh_.ring + laneOff))) +
+                      8u * static_cast<uint32_t>(slot * GQ + u0);
+        // B fragments read kPF steps ahead of their MFMAs (across period boundaries)
+        constexpr int kPF = (NS >= 2 && GAR_HXS_PF2) ? 2 : 1;
+        h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
+        h8v bh1 = bh0, bl1 = bl0;
+        if constexpr (kPF == 2) { bh1 = bFragA(aH + 256); bl1 = bFragA(aH + dL + 256); }
+        // one period's MFMA program into nA (hi-x products) and nL (lo-x products); the
+        // epilogue of period ep (oA, oL) issues after its second step when epi
+        auto period = [&](f32x4& nA, f32x4& nL, const f32x4& oA, const f32x4& oL, bool epi, int ep, bool last) {
+            asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
+            const uint32_t aL = aH + dL, aN = aH + pstep, aNL = aN + dL;
+            nA = f32x4{0, 0, 0, 0};
+            nL = nA;
 #pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    const int ug = (s + 1) / NS, us = (s + 1) % NS;
-                    h8v bh1 = bh0, bl1 = bl0;
-                    if (!(ug == 1 && last)) {
-                        bh1 = bFragA((ug == 0 ? aH : aN) + 256 * us);
-                        bl1 = bFragA((ug == 0 ? aL : aNL) + 256 * us);
-                    }
-                    nA = mfma16(Ah[s], bh0, nA);
-                    nA = mfma16(Al[s], bh0, nA);
-                    nL = mfma16(Ah[s], bl0, nL);
-                    bh0 = bh1; bl0 = bl1;
-                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (s == (NS > 1 ? 1 : 0) && epi) epilogue(oA, oL, ep);
+            for (int s = 0; s < NS; ++s) {
+                const int ug = (s + kPF) / NS, us = (s + kPF) % NS;
+                h8v bhn = kPF == 2 ? bh1 : bh0, bln = kPF == 2 ? bl1 : bl0;
+                if (!(ug == 1 && last)) {
+                    bhn = bFragA((ug == 0 ? aH : aN) + 256 * us);
+                    bln = bFragA((ug == 0 ? aL : aNL) + 256 * us);
                 }
-                aH = aN;
-            };
-            const int p0 = g * x.G;
-            f32x4 a0, a1 = {0, 0, 0, 0}, l0, l1 = a1;
-            if (x.dbg & 4) {
-                epilogue(a1, l1, p0);
-                if (x.G > 1) epilogue(a1, l1, p0 + 1);
-                if (x.G > 2) epilogue(a1, l1, p0 + 2);
-            } else {
+                nA = mfma16(Ah[s], bh0, nA);
+                nA = mfma16(Al[s], bh0, nA);
+                nL = mfma16(Ah[s], bl0, nL);
+                if constexpr (kPF == 2) {
+                    bh0 = bh1; bl0 = bl1; bh1 = bhn; bl1 = bln;
+                } else {
+                    bh0 = bhn; bl0 = bln;
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (s == (NS > 1 ? 1 : 0) && epi) epilogue(oA, oL, ep);
+            }
+            aH = aN;
+        };
+        const int p0 = g * x.G;
+        f32x4 a0, a1 = {0, 0, 0, 0}, l0, l1 = a1;
+        if (dbg & 4) {
+            epilogue(a1, l1, p0);
+            if (x.G > 1) epilogue(a1, l1, p0 + 1);
+            if (x.G > 2) epilogue(a1, l1, p0 + 2);
+        } else {
             // periods in pairs (alternating accumulators): period i's stores issue from
             // inside period i+1's MFMA stream
             period(a0, l0, a1, l1, false, 0, x.G == 1);
@@ -623,11 +624,54 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             } else {
                 epilogue(a0, l0, p0 + i - 1);
             }
-            }
-            const unsigned long long t1 = x.prof ? __builtin_amdgcn_s_memtime() : 0;
-            hxsBarrier();  // step done: load j in the ring, load j + 1 landed
-            if (x.prof) { tm += t1 - t0; tw += __builtin_amdgcn_s_memtime() - t1; }
         }
+        const unsigned long long t1 = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+        hxsBarrier();  // step done: load j in the ring, load j + 1 landed
+        if (kHxsDev && x.prof) { tm += t1 - t0; tw += __builtin_amdgcn_s_memtime() - t1; }
+    }
+}
+
+template <int NS, int VST>
+__device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh_, int wt, int lane) {
+    const uint32_t QS = sh_.QS;
+    const int GQ = x.G * x.Qc;
+    const int grp = lane >> 4, l16 = lane & 15;
+    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+    const int* pt = x.progs + kBgProgInts * wt;
+    const int u0 = uni(pt[4]), rbw = uni(pt[3]);
+    const int tid = wt * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    h8v Ah[NS], Al[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
+        Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
+    }
+    const bool fullRb = (rbw + 1) * 16 <= x.Pc;
+    const int nslot = x.R / GQ;
+    unsigned long long tm = 0, tw = 0;
+    const int P = x.small ? 0 : (x.Wg + GQ - 1) / GQ;
+    const int64_t pstride = static_cast<int64_t>(x.Pc) * x.out_fs;
+
+    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+        const int b = hxsBlock(x, bi);
+        hxsBarrier();  // loud state reset; the previous block's ring reads done
+        if (x.small) hxsSmallStage(&x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
+        hxsBarrier();  // load 0 landed (small: the whole window in the ring)
+        const int col = b * 16 + l16;
+        const bool colOk = col < x.ncols;
+        const int kcol = col / x.C, ccol = col - kcol * x.C;
+        const int64_t aCol = x.a_lo + static_cast<int64_t>(kcol) * x.Np;
+        const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;  // first row of this lane's accumulator
+        const bool laneFast = fullRb && colOk && (!x.out_pcm || VST == 4) && aCol + x.Np <= x.a_hi &&
+                              aCol * x.Pc >= x.o_lo && (aCol + x.Np) * x.Pc <= x.o_hi;
+        char* obase = x.out + (aCol * x.Pc + oRow0 + (((VST == 2 || VST == 4) && (lane & 1)) ? 2 : 0)) * x.out_fs +
+                      ((VST == 2 || VST == 4) ? 0 : ccol * x.out_cs);
+        if (__builtin_amdgcn_ballot_w64(!laneFast) == 0)
+            hxsGroups<NS, VST, true>(x, sh_, lane, Ah, Al, laneOff, u0, P, nslot, obase, pstride, aCol, oRow0, colOk,
+                                     ccol, fullRb, tm, tw);
+        else
+            hxsGroups<NS, VST, false>(x, sh_, lane, Ah, Al, laneOff, u0, P, nslot, obase, pstride, aCol, oRow0, colOk,
+                                      ccol, fullRb, tm, tw);
         if (*sh_.flag) {  // uniform (LDS after the barrier; reset only after the barrier below)
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
             __syncthreads();
@@ -635,11 +679,10 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             __syncthreads();  // every wave's fixup read loudLo/loudHi before the next block resets them
         }
     }
-    if (x.prof && lane == 0) {
+    if (kHxsDev && x.prof && lane == 0) {
         atomicAdd(x.prof + 4, tm);
         atomicAdd(x.prof + 5, tw);
         atomicAdd(x.prof + 6, 1ull);
-        atomicAdd(x.prof + 15, tcv);
     }
 }
 
@@ -673,7 +716,7 @@ __device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared
             for (int d = 0; d < kHxsD; ++d) {
                 const int j = j0 + d;
                 xp = hxsCold();
-                const int dbg = xp->dbg;
+                const int dbg = kHxsDev ? xp->dbg : 0;
                 if ((dbg & 64) && j >= P) {  // development: consume the registers, no conversion
                     float s = 0.f;
 #pragma unroll
@@ -742,7 +785,7 @@ hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t s
     return hipGetLastError();
 }
 
-#define GAR_HXS_FOR4(M, NS) M(NS, 0) M(NS, 1) M(NS, 2) M(NS, 3)
+#define GAR_HXS_FOR4(M, NS) M(NS, 0) M(NS, 1) M(NS, 2) M(NS, 3) M(NS, 4)
 #define GAR_HXS_FOR_LO(M) GAR_HXS_FOR4(M, 1) GAR_HXS_FOR4(M, 2) GAR_HXS_FOR4(M, 3) GAR_HXS_FOR4(M, 4) GAR_HXS_FOR4(M, 5)
 #define GAR_HXS_FOR_HI(M) GAR_HXS_FOR4(M, 6) GAR_HXS_FOR4(M, 7) GAR_HXS_FOR4(M, 8) GAR_HXS_FOR4(M, 9) GAR_HXS_FOR4(M, 10)
 #define GAR_HXS_FOR_ALL(M) GAR_HXS_FOR_LO(M) GAR_HXS_FOR_HI(M)

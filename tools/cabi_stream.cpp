@@ -99,8 +99,8 @@ int main(int argc, char** argv) {
     }
     printf("{\"mode\": \"device_enqueue_only\", \"us_per_call\": %.2f}\n", tq / calls * 1e6);
 
-    // host C-ABI (ProcessMulti over planar float64), bounded to 15 s
-    const int64_t hf = std::min<int64_t>(frames, 15 * 44100);
+    // host C-ABI (ProcessMulti over planar float64), bounded to 15 s (3 s at >= 64 channels)
+    const int64_t hf = std::min<int64_t>(frames, (C >= 64 ? 3 : 15) * 44100);
     std::vector<std::vector<double>> in(C, std::vector<double>(hf)), out(C, std::vector<double>(chunk * 2 + 64));
     for (int c = 0; c < C; ++c)
         for (int64_t t = 0; t < hf; ++t) in[c][t] = xh[t * C + c];
@@ -124,5 +124,27 @@ int main(int argc, char** argv) {
     printf("{\"mode\": \"host_multi_f64\", \"chunk\": %d, \"calls\": %lld, \"us_per_call\": %.2f, \"msamples_per_s\": %.2f}\n",
            chunk, (long long)hcalls, (h1 - h0) / hcalls * 1e6, hf * C / (h1 - h0) / 1e6);
     gar_free(r);
+
+    // the reference's own ProcessInto benchmark shape (processinto_bench_test.go:30-47): NewEngine
+    // 48k->16k QualityMedium, Reset + ProcessInto of 3 s of mono float64 per iteration
+    gar_resampler* e = nullptr;
+    CK(gar_new_engine(48000, 16000, GAR_QUALITY_MEDIUM, GAR_F64, &e));
+    std::vector<double> min(48000 * 3), mout(gar_estimate_output(e, 48000 * 3));
+    for (size_t i = 0; i < min.size(); ++i) min[i] = static_cast<double>(i) * 1e-5;
+    auto monoPass = [&]() {
+        gar_reset(e);
+        int64_t got = 0;
+        CK(gar_process_into_f64(e, min.data(), static_cast<int64_t>(min.size()), mout.data(),
+                                static_cast<int64_t>(mout.size()), &got));
+        return got;
+    };
+    for (int i = 0; i < 3; ++i) monoPass();
+    const int iters = 200;
+    const double m0 = now();
+    for (int i = 0; i < iters; ++i) monoPass();
+    const double m1 = now();
+    printf("{\"mode\": \"engine_processinto_48k_16k_medium_3s\", \"us_per_call\": %.2f, \"msamples_per_s\": %.2f}\n",
+           (m1 - m0) / iters * 1e6, 48000.0 * 3 * iters / (m1 - m0) / 1e6);
+    gar_free(e);
     return 0;
 }
