@@ -243,8 +243,11 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const int64_t blocks = x.nblocks;
     switch (p.NS) {
 #define GAR_HXS_NS(n) case n: return hxsVst<n>(x, lds, blocks, stream);
+#if !GAR_HXS_QUICK
         GAR_HXS_NS(1) GAR_HXS_NS(2) GAR_HXS_NS(3) GAR_HXS_NS(4) GAR_HXS_NS(5) GAR_HXS_NS(6) GAR_HXS_NS(7)
-        GAR_HXS_NS(8) GAR_HXS_NS(9) GAR_HXS_NS(10)
+        GAR_HXS_NS(8)
+#endif
+        GAR_HXS_NS(9) GAR_HXS_NS(10)
 #undef GAR_HXS_NS
         default: return hipErrorNotSupported;
     }

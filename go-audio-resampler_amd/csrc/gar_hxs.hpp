@@ -52,6 +52,12 @@ constexpr int kHxsItems = (4 * kHxsNP + kHxsLoaders - 1) / kHxsLoaders;  // (qua
 #define GAR_HXS_DEV 0
 #endif
 constexpr bool kHxsDev = GAR_HXS_DEV != 0;
+#ifndef GAR_HXS_QUICK
+#define GAR_HXS_QUICK 0
+#endif
+#ifndef GAR_HXS_PRIO
+#define GAR_HXS_PRIO 0
+#endif
 #ifndef GAR_HXS_PF2
 #define GAR_HXS_PF2 0  // B fragments two steps ahead (A/B builds)
 #endif
@@ -358,7 +364,9 @@ __device__ __forceinline__ HxsRegSrc hxsRegSrc(XP x, int b, int lane) {
     r.rowB = static_cast<int>(x->in_fs) * x->in_esz;
     r.chunkB = x->Np * x->Qc * r.rowB;
     r.r = hxsRsrcT(x, hxsChunkRow(x, k, 0), FMT == 2 ? c0 : 0, FMT == 2 ? 64 : (FMT == 3 ? 4 : 8));
-    r.lane0 = lane * r.rowB;
+    // ROW16: lane = 16 q + r reads row r of a 16-row piece, channels 4q..4q+3 -- one instruction
+    // covers 16 whole 64-B block rows (16 lines) instead of 16 B of 64 rows (64 lines)
+    r.lane0 = FMT == 2 ? (lane & 15) * r.rowB + 16 * (lane >> 4) : lane * r.rowB;
     return r;
 }
 
@@ -376,8 +384,9 @@ __device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const
     for (int k = 0; k < kHxsItems; ++k) {
         const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
         const bool on = it < 4 * kHxsNP && i < npc;
-        if constexpr (FMT == 2) {
-            const int o = on ? base + 64 * i * rs.rowB + 16 * q : static_cast<int>(0x80000000u);
+        if constexpr (FMT == 2) {  // item = 16-row piece (all four quads)
+            const bool on16 = it < 4 * kHxsNP && 16 * it < (fast ? st.nrow : 0);
+            const int o = on16 ? base + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
             r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
         } else if constexpr (FMT == 1 || FMT == 4) {  // f32 / int32 stereo frames
             const int o = on ? base + 64 * i * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
@@ -471,11 +480,13 @@ __device__ __forceinline__ void hxsRegConvert(XP x, const HxsStage& st, bool fas
 #pragma unroll
         for (int k = 0; k < kHxsItems; ++k) {
             const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
-            if (it < 4 * kHxsNP && 64 * i < st.nrow) {  // uniform
+            if constexpr (FMT == 2) {
+                const int row = 16 * it + (lane & 15);
+                if (it < 4 * kHxsNP && 16 * it < st.nrow && row < st.nrow)
+                    hxsPutItem(x, st, p0, lane >> 4, row, r.v[k], sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+            } else if (it < 4 * kHxsNP && 64 * i < st.nrow) {  // uniform
                 f32x4 e;
-                if constexpr (FMT == 2) {
-                    e = r.v[k];
-                } else if constexpr (FMT == 1) {
+                if constexpr (FMT == 1) {
                     e = f32x4{r.a[k].x, r.a[k].y, r.b[k].x, r.b[k].y};
                 } else if constexpr (FMT == 3) {  // int16 pairs -> float64(i) * (1 / 32767) -> f32
                     const uint32_t ua = r.a[k], ub = r.b[k];
@@ -640,6 +651,7 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     const int* pt = x.progs + kBgProgInts * wt;
     const int u0 = uni(pt[4]), rbw = uni(pt[3]);
     const int tid = wt * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    if constexpr (GAR_HXS_PRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXS_PRIO);  // A/B: MFMA waves win VALU arbitration
     h8v Ah[NS], Al[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -786,8 +798,13 @@ hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t s
 }
 
 #define GAR_HXS_FOR4(M, NS) M(NS, 0) M(NS, 1) M(NS, 2) M(NS, 3) M(NS, 4)
+#if GAR_HXS_QUICK  // development A/B builds (tools/hxs_variant.sh): only the BASELINE plans' NS = 9, 10
+#define GAR_HXS_FOR_LO(M) GAR_HXS_FOR4(M, 9)
+#define GAR_HXS_FOR_HI(M) GAR_HXS_FOR4(M, 10)
+#else
 #define GAR_HXS_FOR_LO(M) GAR_HXS_FOR4(M, 1) GAR_HXS_FOR4(M, 2) GAR_HXS_FOR4(M, 3) GAR_HXS_FOR4(M, 4) GAR_HXS_FOR4(M, 5)
 #define GAR_HXS_FOR_HI(M) GAR_HXS_FOR4(M, 6) GAR_HXS_FOR4(M, 7) GAR_HXS_FOR4(M, 8) GAR_HXS_FOR4(M, 9) GAR_HXS_FOR4(M, 10)
+#endif
 #define GAR_HXS_FOR_ALL(M) GAR_HXS_FOR_LO(M) GAR_HXS_FOR_HI(M)
 #define GAR_HXS_INST(NS, V) template hipError_t hxsLaunch<NS, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
 
