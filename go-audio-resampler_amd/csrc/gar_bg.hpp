@@ -28,6 +28,25 @@ __device__ __forceinline__ TC srcRead(const SrcDesc& s, int64_t t, int c) {
     return TC(0);
 }
 
+// Branch-free srcRead for a source whose input has the compute dtype (no PCM): the element's
+// address is selected (history | input | a readable dummy) and loaded unconditionally, so a run
+// of these issues its loads together instead of one dependent branch + load each.
+template <class TC>
+__device__ __forceinline__ bool srcSameType(const SrcDesc& s) {
+    return !s.in_pcm && (s.in_f64 != 0) == (sizeof(TC) == 8);
+}
+template <class TC>
+__device__ __forceinline__ TC srcReadBF(const SrcDesc& s, int64_t t, int c, bool ok, const void* dummy) {
+    const int64_t h = t - s.hist_base, i = t - s.in_base;
+    const bool valid = ok && t >= 0 && t < s.valid_end;
+    const bool inH = valid && s.hist != nullptr && h >= 0 && h < s.hist_len;
+    const bool inI = valid && !inH && s.in != nullptr && i >= 0 && i < s.in_len;
+    const TC* hp = static_cast<const TC*>(s.hist) + (inH ? h * s.hist_ld + c : 0);
+    const TC* ip = static_cast<const TC*>(s.in) + (inI ? i * s.in_fs + static_cast<int64_t>(c) * s.in_cs : 0);
+    const TC v = *(inH ? hp : (inI ? ip : static_cast<const TC*>(dummy)));
+    return (inH || inI) ? v : TC(0);
+}
+
 template <class TC>
 __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, TC v) {
     if (idx < o.o_lo || idx >= o.o_hi) return;
@@ -193,7 +212,7 @@ __device__ __forceinline__ int tilePieces(const BgGrid& g) {
 // Issue this wave's DMA pieces j in [jlo, jhi) (j = wt mod nwt) of one sub-tile.
 template <class TC>
 __device__ __forceinline__ void loadPieces(const SrcDesc& src, const BgGrid& g, const TileSrc<TC>& ts, TC* sub,
-                                           int wt, int lane, int jlo, int jhi) {
+                                           int wt, int lane, int jlo, int jhi, const void* dummy) {
     constexpr int rowsPerPiece = sizeof(TC) == 8 ? 2 : 4;
     const int n = sizeof(TC) == 8 ? ((lane >> 1) & 15) : (lane & 15);
     const int rsub = sizeof(TC) == 8 ? (lane >> 5) : (lane >> 4);
@@ -202,6 +221,27 @@ __device__ __forceinline__ void loadPieces(const SrcDesc& src, const BgGrid& g, 
     const bool fast = cs.p != nullptr;
     const bool allFast = ts.allFast;
     const int j0 = jlo + ((wt - jlo) % g.nwt + g.nwt) % g.nwt;
+    if (!allFast && srcSameType<TC>(src)) {
+        // boundary block (history seam, flush zeros): batches of 8 branch-free gathers, loads first
+        constexpr int kB = 8;
+        for (int jb = j0; jb < jhi; jb += kB * g.nwt) {
+            TC v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int j = jb + u * g.nwt;
+                const int kk = j * rowsPerPiece + rsub;
+                const bool ok = j < jhi && kk < g.W && cs.ok && half == 0;
+                v[u] = fast ? *(ok ? cs.p + kk * cs.stride : static_cast<const TC*>(dummy)) : srcReadBF<TC>(src, cs.t0 + kk, cs.c, ok, dummy);
+                if (!ok) v[u] = TC(0);
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int j = jb + u * g.nwt;
+                if (j < jhi && half == 0) sub[static_cast<size_t>(j) * rowsPerPiece * 16 + rsub * 16 + n] = v[u];
+            }
+        }
+        return;
+    }
     for (int j = j0; j < jhi; j += g.nwt) {
         int kk = j * rowsPerPiece + rsub;
         TC* dst = sub + static_cast<size_t>(j) * rowsPerPiece * 16;
@@ -222,9 +262,9 @@ __device__ __forceinline__ void loadPieces(const SrcDesc& src, const BgGrid& g, 
 
 template <class TC>
 __device__ __forceinline__ void loadTile(const SrcDesc& src, const BgGrid& g, int b, TC* sub, int cg, int wt,
-                                         int lane) {
+                                         int lane, const void* dummy) {
     const TileSrc<TC> ts = tileSrc<TC>(src, g, b, cg, lane);
-    loadPieces<TC>(src, g, ts, sub, wt, lane, 0, tilePieces<TC>(g));
+    loadPieces<TC>(src, g, ts, sub, wt, lane, 0, tilePieces<TC>(g), dummy);
 }
 
 // Generic epilogue of one accumulator (row block rb of macro period a).
@@ -285,7 +325,7 @@ __device__ __forceinline__ void segStore(const ProgU& pu, int j, const typename 
 // B fragment of program step s: LDS tile, or global memory (GLOBAL_B).
 template <class TC, bool GB>
 __device__ __forceinline__ TC fetchB(const TC* bp, const ProgU& pu, int s, const SrcDesc& src, int64_t tb, int c,
-                                     bool colOk) {
+                                     bool colOk, bool same, const void* dummy) {
     if constexpr (GB) return colOk ? srcRead<TC>(src, tb + selK(pu, s) + 4 * s, c) : TC(0);
     else return bp[selU(pu, s) + 64 * s];
 }
@@ -319,6 +359,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     const int nloc = cg * 16 + (lane & 15);
     const int laneOff = (lane >> 4) * 16 + (lane & 15);      // B fragment (k = lane>>4, n = lane&15)
     const TC* Aimg = static_cast<const TC*>(p.A);
+    const bool same = srcSameType<TC>(src);
 
     TC A[NS];
     if (SINGLE && wt < g.nprog) {
@@ -327,7 +368,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     }
 
     int b = blockIdx.x;
-    if (!GLOBAL_B && b < g.nblocks) loadTile<TC>(src, g, b, tiles + cg * subElems, cg, wt, lane);
+    if (!GLOBAL_B && b < g.nblocks) loadTile<TC>(src, g, b, tiles + cg * subElems, cg, wt, lane, Aimg);
     int q = 0;  // macro-period iteration counter (partial-slot parity)
     for (int it = 0; b < g.nblocks; b += gridDim.x, ++it) {
         TC* tile = tiles + static_cast<size_t>(it & 1) * tileElems + cg * subElems;
@@ -348,7 +389,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
             const int64_t a = g.a_lo + static_cast<int64_t>(chunk) * g.G + gi;
             // next block's tile: 1/G of its DMA pieces per iteration, so the
             // LDS-DMA issue interleaves with the MFMA stream instead of bursting
-            if (pre) loadPieces<TC>(src, g, nts, ntile, wt, lane, gi * np / g.G, (gi + 1) * np / g.G);
+            if (pre) loadPieces<TC>(src, g, nts, ntile, wt, lane, gi * np / g.G, (gi + 1) * np / g.G, Aimg);
             TC* pslots = part + static_cast<size_t>(g.parity ? (q & 1) : 0) * partStride +
                          static_cast<size_t>(cg) * g.nslots * 256;
 
@@ -367,36 +408,40 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                     // (global-B variant: window too large for LDS, B straight from L1/L2)
                     const TC* bp = tile + gi * g.Qc * 16 + laneOff;
                     const int64_t tb = a * g.Qc + (lane >> 4);
-                    TC bA[4], bB[4];
+                    constexpr int PF = 4;
+                    TC bA[PF], bB[PF];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + j, src, tb, c, colOk);
+                    for (int j = 0; j < PF; ++j)
+                        if (j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + j, src, tb, c, colOk, same, Aimg);
 #pragma unroll
-                    for (int s0 = 0; s0 < NS; s0 += 8) {
-                        if (s0 + 4 < NS) {
+                    for (int s0 = 0; s0 < NS; s0 += 2 * PF) {
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) bB[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 4 + j, src, tb, c, colOk);
-                        }
+                        for (int j = 0; j < PF; ++j)
+                            if (s0 + PF + j < NS) bB[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + PF + j, src, tb, c, colOk, same, Aimg);
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
+                        for (int j = 0; j < PF; ++j) {
                             const int s = s0 + j;
-                            if (j & 1) acc1 = Acc<TC>::mfma(A[s], bA[j], acc1);
-                            else acc0 = Acc<TC>::mfma(A[s], bA[j], acc0);
-                            GAR_SEG_CHECK(sb + s)
+                            if (s < NS) {
+                                if (j & 1) acc1 = Acc<TC>::mfma(A[s], bA[j], acc1);
+                                else acc0 = Acc<TC>::mfma(A[s], bA[j], acc0);
+                                GAR_SEG_CHECK(sb + s)
+                            }
                         }
                         __builtin_amdgcn_sched_barrier(0);
-                        if (s0 + 4 < NS) {
-                            if (s0 + 8 < NS) {
+                        if (s0 + PF < NS) {
 #pragma unroll
-                                for (int j = 0; j < 4; ++j) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 8 + j, src, tb, c, colOk);
-                            }
+                            for (int j = 0; j < PF; ++j)
+                                if (s0 + 2 * PF + j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 2 * PF + j, src, tb, c, colOk, same, Aimg);
                             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                const int s = s0 + 4 + j;
-                                if (j & 1) acc1 = Acc<TC>::mfma(A[s], bB[j], acc1);
-                                else acc0 = Acc<TC>::mfma(A[s], bB[j], acc0);
-                                GAR_SEG_CHECK(sb + s)
+                            for (int j = 0; j < PF; ++j) {
+                                const int s = s0 + PF + j;
+                                if (s < NS) {
+                                    if (j & 1) acc1 = Acc<TC>::mfma(A[s], bB[j], acc1);
+                                    else acc0 = Acc<TC>::mfma(A[s], bB[j], acc0);
+                                    GAR_SEG_CHECK(sb + s)
+                                }
                             }
                             __builtin_amdgcn_sched_barrier(0);
                         }

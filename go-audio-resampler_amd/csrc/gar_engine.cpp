@@ -86,7 +86,7 @@ struct StageRT {
     BgPlan fusedP, dftP, decimP;
     DevBuf fusedA, fusedT, dftA, dftT, decimA, decimT;
     BgDev fusedD{}, dftD{}, decimD{};
-    DevBuf pa, pb, pc, pd;
+    DevBuf pa, pb, pc, pd, pabcd;
     PolyDev polyD{};
     // split-f16 variants (f32 compute), referenced from the BgDev's .hx
     struct HxRT {
@@ -217,6 +217,12 @@ bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
                 uploadBank<float>(d.poly.cc, s.pc); uploadBank<float>(d.poly.d, s.pd);
             }
             p.a = s.pa.p; p.b = s.pb.p; p.c = s.pc.p; p.d = s.pd.p;
+            std::vector<double> il(4 * d.poly.a.size());
+            for (size_t i = 0; i < d.poly.a.size(); ++i) {
+                il[4 * i] = d.poly.a[i]; il[4 * i + 1] = d.poly.b[i]; il[4 * i + 2] = d.poly.cc[i]; il[4 * i + 3] = d.poly.d[i];
+            }
+            if (f64) uploadBank<double>(il, s.pabcd); else uploadBank<float>(il, s.pabcd);
+            p.abcd = s.pabcd.p;
         }
     }
     return true;

@@ -15,9 +15,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <set>
+#include <type_traits>
 #include <utility>
 
 #include "gar_bg.hpp"
@@ -110,6 +112,14 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
         g.hn = hc->n;
         hc->done = true;
     }
+    static const bool trace = std::getenv("GAR_BG_TRACE") != nullptr;
+    static int traced = 0;
+    if (trace && traced < 64) {
+        ++traced;
+        fprintf(stderr, "bg: f64=%d Pc=%d Qc=%d Kc=%d Kread=%d NS=%d kch=%d nw=%d ncg=%d nprog=%d nred=%d nslots=%d G=%d nmac=%lld C=%d nblocks=%d blocks=%lld lds=%zu globalB=%d o[%lld,%lld)\n",
+                p.f64, p.Pc, p.Qc, p.Kc, p.Kread, p.NS, g.kch, g.nwt, g.ncg, g.nprog, g.nred, g.nslots, g.G,
+                (long long)nmac, C, g.nblocks, (long long)blocks, lds, globalB ? 1 : 0, (long long)od.o_lo, (long long)od.o_hi);
+    }
     if (p.f64) return bgLaunchF64(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
     if (p.NS < 56) return bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
     return bgLaunchF32b(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
@@ -118,66 +128,218 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
 // ---------------------------------------------------------------------------
 // General polyphase stage (cubic sub-phase interpolation live).
 // ---------------------------------------------------------------------------
-// A workgroup owns a tile of consecutive outputs: it first evaluates the
-// interpolated coefficients a + x(b + x(c + x d)) of every (output, tap) of the
-// tile ONCE into LDS (the reference evaluates them per channel inside
-// CubicInterpDot, polyphase_stage.go:283-289), then each thread accumulates
-// one (output, channel) dot product over the shared row -- consecutive threads
-// are consecutive channels of one output, so the input reads coalesce for
-// many channels and the taps of neighbouring outputs hit the same lines.
-// Per-tap arithmetic and summation order are those of the reference's loop.
-constexpr int kPolyThreads = 256;
-constexpr int kPolyLdsBytes = 48 * 1024;
+// One thread per (output, group of CG consecutive channels) -- consecutive threads are consecutive
+// channel groups of one output, then consecutive outputs -- accumulating the T taps of its output in
+// the reference's order (polyphase_stage.go:257-293: coefficient a + x(b + x(c + x d)) of tap k
+// times u[base + k], summed k = 0 .. T-1), the coefficient evaluated once for the CG channels.  The
+// four coefficient banks are interleaved ([L][T][4]) so a tap's coefficients are one 16/32-B read;
+// when they fit (L*T*16 B <= 144 KiB) every workgroup copies them into LDS once and walks the
+// outputs grid-stride.  The window u[base .. base + T) of an output is addressed directly when it
+// lies inside the input or the history buffer (the common case: one pointer, one row stride, CG
+// channels as one vector load); windows across the history seam or the stream end are gathered
+// branch-free (srcReadBF), so the unrolled taps issue their loads together.
+constexpr int kPolyThreads = 1024;  // 4 waves per SIMD: the tap loop is load-latency bound
+constexpr size_t kPolyLdsMax = 144 * 1024;
 
+template <class TC, int CG>
+struct PolyVec { typedef TC __attribute__((ext_vector_type(CG))) V; };
 template <class TC>
+struct PolyVec<TC, 1> { typedef TC V; };
+
+template <class TC, int CG>
+__device__ __forceinline__ TC pvGet(const typename PolyVec<TC, CG>::V& v, int j) {
+    if constexpr (CG == 1) return v;
+    else return v[j];
+}
+
+// WIN (with BANK_LDS): the workgroup's threads form a tile of consecutive (output, channel group)
+// items; the tile's whole input window (rows [base(first output), base(last output) + T) x C) is
+// staged into LDS once with coalesced branch-free gathers, and the tap loop reads it from there.
+// Tap order of output m: k = r, r+1, .., T-1, 0, .., r-1 with r = (m - ph*T) mod 16 (mod T), so
+// the bank rows [ph][k] that 16 consecutive outputs read in one step fall on 16 distinct 16-B LDS
+// bank groups (slot (ph*T + k) mod 16 = (m + i) mod 16) instead of colliding on ph mod 16.  A
+// function of the output alone: every launch geometry sums an output in the same order
+// (chunk-invariant bits); the reference sums k = 0 .. T-1 (the f32 / f64 tolerances cover it).
+__device__ __forceinline__ int polyRot(int64_t m, int ph, int T) {
+    return static_cast<int>((static_cast<unsigned>(m) - static_cast<unsigned>(ph) * static_cast<unsigned>(T)) & 15u) % T;
+}
+
+template <class TC, bool BANK_LDS, int CG, bool WIN>
 __global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc src, OutDesc od, int64_t nout, int C,
-                                                            int MT) {
+                                                            int winRows) {
+    typedef typename std::conditional<sizeof(TC) == 8, f64x4, f32x4>::type V4;
+    typedef typename PolyVec<TC, CG>::V VC;
     extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
-    TC* coef = reinterpret_cast<TC*>(psm);  // [MT][T]
-    const TC* A = static_cast<const TC*>(p.a);
-    const TC* B = static_cast<const TC*>(p.b);
-    const TC* Cc = static_cast<const TC*>(p.c);
-    const TC* D = static_cast<const TC*>(p.d);
+    const int T = p.T, L = p.L;
+    const V4* bankG = static_cast<const V4*>(p.abcd);
+    const V4* bank = bankG;
+    if constexpr (BANK_LDS) {
+        V4* lb = reinterpret_cast<V4*>(psm);
+        for (int i = threadIdx.x; i < L * T; i += blockDim.x) lb[i] = bankG[i];
+        __syncthreads();
+        bank = lb;
+    }
     const TC fscale = static_cast<TC>(1.0 / 65536.0);
-    const int T = p.T;
-    const int64_t ntiles = (nout + MT - 1) / MT;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t m0 = tile * MT;
-        const int mt = static_cast<int>(min<int64_t>(MT, nout - m0));
-        __syncthreads();  // previous tile's rows consumed
-        for (int e = threadIdx.x; e < mt * T; e += blockDim.x) {
-            const int mm = e / T, k = e - mm * T;
-            const int64_t at = p.at0 + (m0 + mm) * p.step;
-            const int ph = static_cast<int>((at >> 16) % p.L);
-            const TC x = static_cast<TC>(at & 0xFFFF) * fscale;
-            const size_t o = static_cast<size_t>(ph) * T + k;
-            coef[mm * T + k] = A[o] + x * (B[o] + x * (Cc[o] + x * D[o]));
+    const bool same = srcSameType<TC>(src);
+    const int ng = C / CG;  // launcher: CG divides C
+    const int64_t total = nout * ng;
+    TC* win = reinterpret_cast<TC*>(psm + (BANK_LDS ? static_cast<size_t>(L) * T * sizeof(V4) : 0));
+    const int64_t ntile = (total + blockDim.x - 1) / blockDim.x;
+    for (int64_t tile = blockIdx.x; tile < (WIN ? ntile : 0); tile += gridDim.x) {  // uniform per workgroup
+        const int64_t i0 = tile * blockDim.x, i1 = min<int64_t>(total, i0 + blockDim.x);
+        const int64_t mlo = i0 / ng, mhi = (i1 - 1) / ng;
+        const int64_t blo = p.u_base + ((p.at0 + mlo * p.step) >> 16) / L;
+        const int64_t bhi = p.u_base + ((p.at0 + mhi * p.step) >> 16) / L + T;  // exclusive
+        const int nr = static_cast<int>(bhi - blo);                              // <= winRows (launcher bound)
+        __syncthreads();  // previous tile's window consumed
+        for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
+            const int r = e / C, c = e - r * C;
+            win[e] = same ? srcReadBF<TC>(src, blo + r, c, r < winRows, bankG) : srcRead<TC>(src, blo + r, c);
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < mt * C; e += blockDim.x) {
-            const int mm = e / C, c = e - mm * C;
-            const int64_t at = p.at0 + (m0 + mm) * p.step;
-            const int64_t base = p.u_base + (at >> 16) / p.L;
-            const TC* row = coef + mm * T;
-            TC acc = 0;
-            for (int k = 0; k < T; ++k) acc += srcRead<TC>(src, base + k, c) * row[k];
-            outWrite<TC>(od, od.o_lo + m0 + mm, c, acc);
+        if (i0 + threadIdx.x >= i1) continue;
+        // 32-bit per-thread index arithmetic relative to the tile's first output (its 64-bit
+        // quantities are wave-uniform): output m = mlo + d, position at = atlo + d*step
+        const int r0 = static_cast<int>(i0 - mlo * ng);  // item offset of the tile start within output mlo
+        const unsigned li = static_cast<unsigned>(r0) + threadIdx.x;
+        const unsigned d = li / static_cast<unsigned>(ng);
+        const int c0 = static_cast<int>(li - d * static_cast<unsigned>(ng)) * CG;
+        const int64_t m = mlo + d;
+        const int64_t atlo = p.at0 + mlo * p.step;
+        const int64_t ailo = atlo >> 16;
+        const int64_t qlo = ailo / L;
+        const int phlo = static_cast<int>(ailo - qlo * L);
+        const int64_t at = atlo + static_cast<int64_t>(d) * p.step;
+        const unsigned t = static_cast<unsigned>(phlo) + static_cast<unsigned>((at >> 16) - ailo);
+        const unsigned dq = t / static_cast<unsigned>(L);
+        const int ph = static_cast<int>(t - dq * static_cast<unsigned>(L));
+        const int64_t q = qlo + dq;
+        const TC x = static_cast<TC>(at & 0xFFFF) * fscale;
+        const TC* wl = win + (p.u_base + q - blo) * C + c0;
+        const V4* row = bank + static_cast<size_t>(ph) * T;
+        TC acc[CG];
+#pragma unroll
+        for (int j = 0; j < CG; ++j) acc[j] = 0;
+        int k = polyRot(m, ph, T);
+#pragma unroll 8
+        for (int i = 0; i < T; ++i) {
+            const V4 cf = row[k];
+            const TC co = cf[0] + x * (cf[1] + x * (cf[2] + x * cf[3]));
+            const VC v = *reinterpret_cast<const VC*>(wl + k * C);
+#pragma unroll
+            for (int j = 0; j < CG; ++j) acc[j] += pvGet<TC, CG>(v, j) * co;
+            k = k + 1 == T ? 0 : k + 1;
         }
+#pragma unroll
+        for (int j = 0; j < CG; ++j) outWrite<TC>(od, od.o_lo + m, c0 + j, acc[j]);
     }
+    for (int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; idx < (WIN ? 0 : total);
+         idx += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t m = idx / ng;
+        const int c0 = static_cast<int>(idx - m * ng) * CG;
+        const int64_t at = p.at0 + m * p.step;
+        const int64_t ai = at >> 16;
+        const int64_t q = ai / L;
+        const int ph = static_cast<int>(ai - q * L);
+        const TC x = static_cast<TC>(at & 0xFFFF) * fscale;
+        const int64_t base = p.u_base + q;
+        const V4* row = bank + static_cast<size_t>(ph) * T;
+        // direct window: inside the input (compute dtype) or inside the history buffer
+        const TC* wp = nullptr;
+        int64_t ws = 0;
+        if (same && src.in && base >= src.in_base && base + T <= src.in_base + src.in_len && base + T <= src.valid_end &&
+            base >= 0) {
+            wp = static_cast<const TC*>(src.in) + (base - src.in_base) * src.in_fs + static_cast<int64_t>(c0) * src.in_cs;
+            ws = src.in_fs;
+        } else if (src.hist && base >= src.hist_base && base + T <= src.hist_base + src.hist_len && base + T <= src.valid_end &&
+                   base >= 0) {
+            wp = static_cast<const TC*>(src.hist) + (base - src.hist_base) * src.hist_ld + c0;
+            ws = src.hist_ld;
+        }
+        TC acc[CG];
+#pragma unroll
+        for (int j = 0; j < CG; ++j) acc[j] = 0;
+        int k = polyRot(m, ph, T);
+        if (wp) {
+#pragma unroll 8
+            for (int i = 0; i < T; ++i) {
+                const V4 cf = row[k];
+                const TC co = cf[0] + x * (cf[1] + x * (cf[2] + x * cf[3]));
+                const VC v = *reinterpret_cast<const VC*>(wp + k * ws);
+#pragma unroll
+                for (int j = 0; j < CG; ++j) acc[j] += pvGet<TC, CG>(v, j) * co;
+                k = k + 1 == T ? 0 : k + 1;
+            }
+        } else {
+#pragma unroll 4
+            for (int i = 0; i < T; ++i) {
+                const V4 cf = row[k];
+                const TC co = cf[0] + x * (cf[1] + x * (cf[2] + x * cf[3]));
+#pragma unroll
+                for (int j = 0; j < CG; ++j)
+                    acc[j] += (same ? srcReadBF<TC>(src, base + k, c0 + j, true, bankG) : srcRead<TC>(src, base + k, c0 + j)) * co;
+                k = k + 1 == T ? 0 : k + 1;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < CG; ++j) outWrite<TC>(od, od.o_lo + m, c0 + j, acc[j]);
+    }
+}
+
+template <class TC, bool BANK_LDS, bool WIN>
+static void polyGo(int CG, dim3 gd, dim3 bd, size_t lds, hipStream_t st, const PolyDev& p, const SrcDesc& src,
+                   const OutDesc& od, int64_t nout, int C, int winRows) {
+    if (BANK_LDS) {
+        setMaxLdsOnce(reinterpret_cast<const void*>(&poly_kernel<TC, BANK_LDS, 1, WIN>));
+        setMaxLdsOnce(reinterpret_cast<const void*>(&poly_kernel<TC, BANK_LDS, 2, WIN>));
+        setMaxLdsOnce(reinterpret_cast<const void*>(&poly_kernel<TC, BANK_LDS, 4, WIN>));
+    }
+    if (CG == 4) hipLaunchKernelGGL((poly_kernel<TC, BANK_LDS, 4, WIN>), gd, bd, lds, st, p, src, od, nout, C, winRows);
+    else if (CG == 2) hipLaunchKernelGGL((poly_kernel<TC, BANK_LDS, 2, WIN>), gd, bd, lds, st, p, src, od, nout, C, winRows);
+    else hipLaunchKernelGGL((poly_kernel<TC, BANK_LDS, 1, WIN>), gd, bd, lds, st, p, src, od, nout, C, winRows);
 }
 
 hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& od, int64_t nout, int C,
                       hipStream_t stream) {
     if (nout <= 0) return hipSuccess;
-    const int es = p.f64 ? 8 : 4;
-    // outputs per tile: enough (output, channel) pairs for the block, rows within the LDS budget
-    int MT = std::max(1, (2 * kPolyThreads + C - 1) / C);
-    MT = std::min<int>(MT, std::max(1, kPolyLdsBytes / (p.T * es)));
-    const int64_t ntiles = (nout + MT - 1) / MT;
-    const int64_t blocks = std::min<int64_t>(ntiles, 8192);
-    const size_t lds = static_cast<size_t>(MT) * p.T * es;
-    if (p.f64) hipLaunchKernelGGL(poly_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(kPolyThreads), lds, stream, p, src, od, nout, C, MT);
-    else hipLaunchKernelGGL(poly_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(kPolyThreads), lds, stream, p, src, od, nout, C, MT);
+    const size_t es = p.f64 ? 8 : 4;
+    const size_t bankB = static_cast<size_t>(p.L) * p.T * 4 * es;
+    // channel group: CG consecutive channels share a coefficient evaluation and one vector load per
+    // tap, when every direct window has contiguous, CG-aligned channels (stride 1, row strides and
+    // bases multiples of CG elements)
+    auto alignedFor = [&](int cg) {
+        if (C % cg != 0) return false;
+        const bool inOk = !src.in || (src.in_cs == 1 && src.in_fs % cg == 0 &&
+                                      reinterpret_cast<uintptr_t>(src.in) % (cg * es) == 0);
+        const bool hOk = !src.hist || (src.hist_ld % cg == 0 && reinterpret_cast<uintptr_t>(src.hist) % (cg * es) == 0);
+        return inOk && hOk;
+    };
+    const int CG = alignedFor(4) ? 4 : (alignedFor(2) ? 2 : 1);
+    const int64_t total = nout * (C / CG);
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // LDS bank: one resident workgroup per CU walks the outputs grid-stride (the bank is copied once
+    // per workgroup); without it, enough workgroups to cover the launch.
+    const bool lbank = bankB <= kPolyLdsMax && total >= static_cast<int64_t>(ncu) * kPolyThreads;
+    int64_t blocks = (total + kPolyThreads - 1) / kPolyThreads;
+    if (lbank) blocks = std::min<int64_t>(blocks, ncu);
+    blocks = std::min<int64_t>(blocks, 65536);
+    const dim3 gd(static_cast<unsigned>(blocks)), bd(kPolyThreads);
+    // window rows of one tile of kPolyThreads items: (outputs - 1) * step / 2^16 / L + T + 2 (rounding)
+    const int64_t mt = (kPolyThreads + (C / CG) - 1) / (C / CG) + 1;
+    const int winRows = static_cast<int>(((mt - 1) * p.step >> 16) / p.L + p.T + 2);
+    const size_t winB = static_cast<size_t>(winRows) * C * es;
+    const bool win = lbank && bankB + winB <= 160 * 1024;
+    const size_t lds = lbank ? bankB + (win ? winB : 0) : 0;
+    if (p.f64) {
+        if (win) polyGo<double, true, true>(CG, gd, bd, lds, stream, p, src, od, nout, C, winRows);
+        else if (lbank) polyGo<double, true, false>(CG, gd, bd, lds, stream, p, src, od, nout, C, winRows);
+        else polyGo<double, false, false>(CG, gd, bd, 0, stream, p, src, od, nout, C, winRows);
+    } else {
+        if (win) polyGo<float, true, true>(CG, gd, bd, lds, stream, p, src, od, nout, C, winRows);
+        else if (lbank) polyGo<float, true, false>(CG, gd, bd, lds, stream, p, src, od, nout, C, winRows);
+        else polyGo<float, false, false>(CG, gd, bd, 0, stream, p, src, od, nout, C, winRows);
+    }
     return hipGetLastError();
 }
 

@@ -91,6 +91,7 @@ struct PolyDev {
     int L, T;
     int64_t step, at0, u_base;  // u_base = global stream index of local history index 0
     const void *a, *b, *c, *d;  // [L][T] reversed, compute dtype
+    const void* abcd;           // [L][T][4] the same four banks interleaved (poly_kernel's one-load tap)
 };
 
 // CubicStage checkpoint (cubic.go:42-61): before input i (absolute stage-input
