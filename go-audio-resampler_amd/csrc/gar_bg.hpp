@@ -74,6 +74,7 @@ struct BgGrid {
     int C, nprog, kch, nwt, ncg, nred, nslots, parity;
     int dbg;  // development timing knob (GAR_BG_DBG): 1 skip tile DMA after the first, 2 skip stores
     int vst;  // f32 epilogue: 0 scalar, 1 channel-contiguous (fs == 1), 2 stereo interleaved (C == 2, fs == 2, cs == 1)
+    int rbMode;  // small launch of a row-block-aligned plan: bg_rb_kernel (G = 1)
     void* hdst;       // folded history keep (HistCopy): hdst[(t - ht0) * C + c] = src(t, c), t < ht0 + hn
     int64_t ht0, hn;
 };
@@ -478,6 +479,97 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     }
 }
 
+// Small launches of row-block-aligned plans (BgPlan::rbAligned): workgroup v = (column block
+// v / nrb, row block v % nrb), one macro period per column (G = 1); wave w runs program
+// rbStart[rb] + w: its A fragments are loaded once, every B fragment of its K piece is fetched up
+// front (one memory round trip: a direct pointer when the piece's rows lie in one buffer), the MFMAs
+// accumulate exactly as in bg_kernel (acc0/acc1 by step parity), and the row block's pieces are
+// summed in program order through LDS -- the persistent kernel's sums, bit for bit, so streams give
+// the same output however they are chunked.  The launch is latency-bound (a 4800-frame f64 chunk
+// is a few dozen tiles): many small workgroups, each one round trip deep, instead of a few
+// workgroups walking every row block.
+// History keep of a bg_rb_kernel launch (the `copy(history, history[consumed:])` of the stage):
+// element i of the new history is copied by thread i (mod the grid) of the flattened grid, issued right after the program's A / B loads so its memory round trip overlaps theirs.
+template <class TC>
+__device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g) {
+    if (g.hn <= 0) return;
+    const int64_t total = g.hn * g.C;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t t = i / g.C;
+        static_cast<TC*>(g.hdst)[i] = srcRead<TC>(src, g.ht0 + t, static_cast<int>(i - t * g.C));
+    }
+}
+
+template <class TC, int NS>
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+    typedef typename Acc<TC>::V V;
+    __shared__ V slots[kBgRbMaxWaves][64];
+    const int lane = threadIdx.x & 63;
+    const int wt = threadIdx.x >> 6;
+    const TC* Aimg = static_cast<const TC*>(p.A);
+    const int nv = g.nblocks * p.nrb;
+    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
+        const int b = v / p.nrb, rb = v - b * p.nrb;
+        const int ps = p.rbStart[rb], np = p.rbStart[rb + 1] - ps;
+        const int col = b * 16 + (lane & 15);
+        const bool colOk = col < g.ncols;
+        const int c = colOk ? col % g.C : 0;
+        const int64_t a = g.a_lo + (colOk ? col / g.C : 0);  // G = 1
+        V r = {0, 0, 0, 0};
+        if (wt < np) {
+            const int pr = ps + wt;
+            const ProgU pu = progLoad(p.progs + kBgProgInts * pr);
+            TC A[NS], B[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+            // rows of this lane: t0 + 4 s, s < NS (the zero-A tail steps read finite rows too)
+            const int64_t t0 = a * g.Qc + pu.k0 + (lane >> 4);
+            const int64_t lo = a * g.Qc + pu.k0, hi = lo + 4 * NS;
+            const TC* dp = nullptr;
+            int64_t ds = 0;
+            if (colOk && hi <= src.valid_end && lo >= 0) {
+                if (srcSameType<TC>(src) && src.in && lo >= src.in_base && hi <= src.in_base + src.in_len) {
+                    dp = static_cast<const TC*>(src.in) + (t0 - src.in_base) * src.in_fs + static_cast<int64_t>(c) * src.in_cs;
+                    ds = 4 * src.in_fs;
+                } else if (src.hist && lo >= src.hist_base && hi <= src.hist_base + src.hist_len) {
+                    dp = static_cast<const TC*>(src.hist) + (t0 - src.hist_base) * src.hist_ld + c;
+                    ds = 4 * src.hist_ld;
+                }
+            }
+            if (dp) {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) B[s] = dp[s * ds];
+            } else {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) B[s] = colOk ? srcRead<TC>(src, t0 + 4 * s, c) : TC(0);
+            }
+            if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside A / B's
+            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+            }
+            r = acc0 + acc1;
+            if (np > 1) slots[wt][lane] = r;
+        }
+        if (np > 1) {
+            __syncthreads();
+            if (wt == 0) {
+                V sum = slots[0][lane];
+                for (int k = 1; k < np; ++k) sum += slots[k][lane];
+                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            }
+            __syncthreads();  // slots free for the next (column block, row block)
+        } else if (wt == 0 && !(g.dbg & 2)) {
+            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        }
+    }
+    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;  // the first (column block, row block) of this workgroup
+    if (wt >= p.rbStart[rb0 + 1] - p.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
+}
+
 template <class TC, int NS>
 static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                              size_t lds, int64_t blocks, hipStream_t st, bool globalB) {
@@ -485,9 +577,17 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
     setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, false, false>));
     setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, true>));
     setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, false>));
-    if (threads > bgMaxThreads(sizeof(TC) == 8, NS)) return hipErrorInvalidConfiguration;
     const dim3 gd(static_cast<unsigned>(blocks)), bd(threads);
-    const bool single = g.kch == 1;
+    if (g.rbMode) {
+        if constexpr (sizeof(TC) == 8 && NS <= kBgRbMaxSteps) {
+            if (threads > 64 * kBgRbMaxWaves) return hipErrorInvalidConfiguration;
+            hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
+            return hipGetLastError();
+        }
+        return hipErrorNotSupported;
+    }
+    if (threads > bgMaxThreads(sizeof(TC) == 8, NS)) return hipErrorInvalidConfiguration;
+    const bool single = g.kch == 1 && g.nprog <= g.nwt;  // one program per wave: A loaded once
     if (globalB) {
         if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, true, true>), gd, bd, lds, st, p, src, od, g);
         else hipLaunchKernelGGL((bg_kernel<TC, NS, true, false>), gd, bd, lds, st, p, src, od, g);

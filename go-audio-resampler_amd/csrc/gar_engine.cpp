@@ -163,16 +163,22 @@ BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
     d.ncg = p.ncg;
     d.nred = static_cast<int>(p.reds.size());
     d.nslots = p.nslots;
+    d.rbAligned = p.rbAligned ? 1 : 0;
+    for (size_t rb = 0; p.rbAligned && rb + 1 < p.rbStart.size(); ++rb)
+        d.maxPrb = std::max(d.maxPrb, p.rbStart[rb + 1] - p.rbStart[rb]);
     if (dry) return d;
     if (p.f64) A.upload(p.A64); else A.upload(p.A32);
     std::vector<int> t = p.progTable();
     const std::vector<int> rt = p.redTable();
     const size_t redOff = t.size();
     t.insert(t.end(), rt.begin(), rt.end());
+    const size_t rbOff = t.size();
+    t.insert(t.end(), p.rbStart.begin(), p.rbStart.end());
     T.upload(t);
     d.A = A.p;
     d.progs = static_cast<const int*>(T.p);
     d.reds = static_cast<const int*>(T.p) + redOff;
+    d.rbStart = p.rbAligned ? static_cast<const int*>(T.p) + rbOff : nullptr;
     return d;
 }
 

@@ -36,6 +36,10 @@ unsigned long long* profBuf() {
                     fprintf(stderr, "hxs prof per wave (cycles): loaders convert %.0f issue+wait %.0f (issue %.0f) barrier %.0f (life %.1f us) | compute convert+mfma %.0f barrier %.0f\n",
                             h[0] / nl, h[1] / nl, h[7] / nl, h[2] / nl, h[9] / nl / 100.0, h[4] / nc, h[5] / nc);
                     fprintf(stderr, "hxs loader pre-loop %.2f us, post-loop %.2f us; compute convert %.0f\n", h[8] / nl / 100.0, h[12] / nl / 100.0, h[15] / nc);
+                    if (h[23]) fprintf(stderr, "hxs wave-0 first block (cycles): entry->window %.0f, window->steps done %.0f, ->exit (stores drained) %.0f, n %llu\n",
+                                       static_cast<double>(h[20]) / h[23], static_cast<double>(h[21]) / h[23], static_cast<double>(h[22]) / h[23], h[23]);
+                    if (h[23]) fprintf(stderr, "hxs wave-0: entry->A landed %.0f, entry->barrier 1 %.0f; wave entry spread in a workgroup %.0f, wave 0 after first wave %.0f\n",
+                                       static_cast<double>(h[24]) / h[23], static_cast<double>(h[25]) / h[23], static_cast<double>(h[26]) / h[23], static_cast<double>(h[27]) / h[23]);
                     fprintf(stderr, "hxs span: first start -> last end %.1f us; loader wave life min %.1f max %.1f us\n",
                             (h[11] - h[10]) / 100.0, h[13] / 100.0, h[14] / 100.0);
                     // per-workgroup life (last launch): percentiles, by blockIdx % 8, slowest

@@ -463,6 +463,7 @@ __device__ __forceinline__ int hxsStepsPad(const HxsArgs& x) {
 }
 
 struct HxsShared {
+    unsigned long long* stamp;
     char* ring;
     uint32_t QS;
     int* loudLo;
@@ -651,12 +652,19 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     const int* pt = x.progs + kBgProgInts * wt;
     const int u0 = uni(pt[4]), rbw = uni(pt[3]);
     const int tid = wt * 64 + lane, nth = 64 * (x.nprog + kHxsLoaders);
+    const unsigned long long tEntry = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tGath = 0, tSteps = 0;
     if constexpr (GAR_HXS_PRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXS_PRIO);  // A/B: MFMA waves win VALU arbitration
     h8v Ah[NS], Al[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
         Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
+    }
+    unsigned long long tA = 0, tB1 = 0;
+    if (kHxsDev && x.prof && wt == 0) {  // development: A landed (an extra wait, stamp only)
+        __builtin_amdgcn_s_waitcnt(0);
+        tA = __builtin_amdgcn_s_memtime();
     }
     const bool fullRb = (rbw + 1) * 16 <= x.Pc;
     const int nslot = x.R / GQ;
@@ -667,8 +675,10 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
         hxsBarrier();  // loud state reset; the previous block's ring reads done
+        if (kHxsDev && x.prof && bi == static_cast<int>(blockIdx.x)) tB1 = __builtin_amdgcn_s_memtime();
         if (x.small) hxsSmallStage(&x, b, tid, nth, sh_.ring, QS, sh_.loudLo, sh_.loudHi, sh_.flag);
         hxsBarrier();  // load 0 landed (small: the whole window in the ring)
+        if (kHxsDev && x.prof && bi == static_cast<int>(blockIdx.x)) tGath = __builtin_amdgcn_s_memtime();
         const int col = b * 16 + l16;
         const bool colOk = col < x.ncols;
         const int kcol = col / x.C, ccol = col - kcol * x.C;
@@ -684,6 +694,7 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
         else
             hxsGroups<NS, VST, false>(x, sh_, lane, Ah, Al, laneOff, u0, P, nslot, obase, pstride, aCol, oRow0, colOk,
                                       ccol, fullRb, tm, tw);
+        if (kHxsDev && x.prof && bi == static_cast<int>(blockIdx.x)) tSteps = __builtin_amdgcn_s_memtime();
         if (*sh_.flag) {  // uniform (LDS after the barrier; reset only after the barrier below)
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
             __syncthreads();
@@ -691,10 +702,37 @@ __device__ __forceinline__ void hxsCompute(const HxsArgs& x, const HxsShared& sh
             __syncthreads();  // every wave's fixup read loudLo/loudHi before the next block resets them
         }
     }
+    if (kHxsDev && x.prof && wt == 0 && lane == 0) {  // development: first-block phase stamps of wave 0
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tExit = __builtin_amdgcn_s_memtime();
+        atomicAdd(x.prof + 20, tGath - tEntry);
+        atomicAdd(x.prof + 21, tSteps - tGath);
+        atomicAdd(x.prof + 22, tExit - tSteps);
+        atomicAdd(x.prof + 23, 1ull);
+        atomicAdd(x.prof + 24, tA - tEntry);
+        atomicAdd(x.prof + 25, tB1 - tEntry);
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int w = 0; w < x.nprog + kHxsLoaders; ++w) { lo = min(lo, sh_.stamp[w]); hi = max(hi, sh_.stamp[w]); }
+        atomicAdd(x.prof + 26, hi - lo);
+        atomicAdd(x.prof + 27, tEntry - lo);
+    }
     if (kHxsDev && x.prof && lane == 0) {
         atomicAdd(x.prof + 4, tm);
         atomicAdd(x.prof + 5, tw);
         atomicAdd(x.prof + 6, 1ull);
+    }
+}
+
+// History keep for the next call (launchGather's job, folded into this launch): hdst is the other
+// buffer of the double-buffered history, so it never aliases what the launch reads.  Large launches:
+// every thread after its role; small launches: the loader waves during the MFMA step (hxsRegLoadersT).
+__device__ __forceinline__ void hxsHistKeep(const HxsArgs& x, int64_t me, int64_t nth) {
+    const HxsArgsP xc = hxsCold();
+    const SrcDesc src = kload(&xc->src);
+    const int64_t total = x.hn * x.C;
+    for (int64_t i = me; i < total; i += nth) {
+        const int64_t t = i / x.C;
+        x.hdst[i] = srcRead<float>(src, x.ht0 + t, static_cast<int>(i - t * x.C));
     }
 }
 
@@ -729,6 +767,9 @@ __device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared
                 const int j = j0 + d;
                 xp = hxsCold();
                 const int dbg = kHxsDev ? xp->dbg : 0;
+                if (xp->small && j == 0 && x.hn > 0 && bi == static_cast<int>(blockIdx.x))  // beside the MFMA group
+                    hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * 64 * kHxsLoaders + 64 * l + lane,
+                                static_cast<int64_t>(gridDim.x) * 64 * kHxsLoaders);
                 if ((dbg & 64) && j >= P) {  // development: consume the registers, no conversion
                     float s = 0.f;
 #pragma unroll
@@ -768,6 +809,13 @@ template <int NS, int VST>
 __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     HxsShared s;
+#if GAR_HXS_DEV
+    __shared__ unsigned long long hxsStamp[kHxsWaves];  // development (GAR_HXS_PROF): wave entry times
+    if (x.prof && (threadIdx.x & 63) == 0) hxsStamp[threadIdx.x >> 6] = __builtin_amdgcn_s_memtime();
+    s.stamp = hxsStamp;
+#else
+    s.stamp = nullptr;
+#endif
     s.QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
     s.ring = reinterpret_cast<char*>(smem);
     s.loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(s.QS));
@@ -775,18 +823,14 @@ __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
     s.flag = s.loudHi + 16;
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
+    // History keep for the next call (launchGather's job, folded into this launch; hdst is the other
+    // buffer of the double-buffered history, so it never aliases what this launch reads).  Small
+    // launches: the loader waves copy it while the compute waves run their MFMAs (the loaders' only
+    // other work is the one-pass window gather); otherwise every thread after its role.
     if (wt < x.nprog) hxsCompute<NS, VST>(x, s, wt, lane);
     else hxsRegLoaders(x, s, wt - x.nprog, lane);
-    if (x.hn > 0) {  // history keep for the next call (launchGather's job, folded into this launch)
-        const HxsArgsP xc = hxsCold();
-        const SrcDesc src = kload(&xc->src);
-        const int64_t total = x.hn * x.C;
-        for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-             i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-            const int64_t t = i / x.C;
-            x.hdst[i] = srcRead<float>(src, x.ht0 + t, static_cast<int>(i - t * x.C));
-        }
-    }
+    if (x.hn > 0 && !x.small) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+                                          static_cast<int64_t>(gridDim.x) * blockDim.x);
 }
 
 // Launch (explicitly instantiated in gar_hxs_i*.hip).

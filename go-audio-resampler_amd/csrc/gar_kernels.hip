@@ -55,6 +55,7 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     static const int knobDbg = std::getenv("GAR_BG_DBG") ? std::atoi(std::getenv("GAR_BG_DBG")) : 0;
     static const bool knobNoVst = std::getenv("GAR_BG_NOVST") != nullptr;
     static const bool knobNoParity = std::getenv("GAR_BG_NOPARITY") != nullptr;
+    g.rbMode = 0;
     g.nprog = p.nprog;
     g.kch = p.kch;
     g.nwt = p.nw;
@@ -64,6 +65,33 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     g.a_lo = od.o_lo / p.Pc;
     const int64_t a_hi = (od.o_hi + p.Pc - 1) / p.Pc;
     const int64_t nmac = a_hi - g.a_lo;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // small launch of a row-block-aligned f64 plan (stream chunks): one (column block, row block) per
+    // workgroup, one macro period per column (bg_rb_kernel) -- same programs, same sums
+    if (p.f64 && p.rbAligned && p.rbStart && (nmac * C + 15) / 16 <= 2 * static_cast<int64_t>(ncu) && !(knobDbg & 8)) {
+        g.rbMode = 1;
+        g.G = 1;
+        g.W = p.Kc;
+        g.Wl = p.Kread;
+        g.Ws = g.Wl;
+        g.nchunk = static_cast<int>(nmac);
+        g.ncols = static_cast<int>(nmac * C);
+        g.nblocks = (g.ncols + 15) / 16;
+        g.dbg = knobDbg;
+        g.vst = 0;
+        g.parity = 0;
+        g.hdst = nullptr;
+        g.ht0 = g.hn = 0;
+        if (hc && hc->n > 0 && hc->dst) {
+            g.hdst = hc->dst;
+            g.ht0 = hc->t0;
+            g.hn = hc->n;
+            hc->done = true;
+        }
+        const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
+        return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, 0, blocks, stream, false);
+    }
     const int threads = 64 * g.ncg * g.nwt;
     const int tileN = 16 * g.ncg;
     const size_t slotBytes = static_cast<size_t>(g.ncg) * g.nslots * 256 * sz;
@@ -101,8 +129,6 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     if (globalB) lds = partBytes;
     if (lds > kLds) return hipErrorInvalidConfiguration;
     if (g.nblocks <= 0) return hipSuccess;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     int64_t blocks = std::min<int64_t>(g.nblocks, static_cast<int64_t>(ncu) * (knobWgPerCu > 0 ? knobWgPerCu : 2));
     g.hdst = nullptr;
     g.ht0 = g.hn = 0;

@@ -59,6 +59,9 @@ struct BgDev {
     const int* progs;   // [nprog][kBgProgInts] (gar_plan.hpp BgPlan::progTable)
     const int* reds;    // [nred][kBgRedInts]
     const HxDev* hx;    // host pointer: split-f16 variant of this plan (f32 compute) or null
+    int rbAligned;      // BgPlan::rbAligned: small launches may run bg_rb_kernel
+    int maxPrb;         // most programs of one row block
+    const int* rbStart; // [nrb + 1]
 };
 
 // Device copy of an HxPlan (gar_plan.hpp): split-f16 MFMA FIR, f32 compute.

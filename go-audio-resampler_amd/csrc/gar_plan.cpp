@@ -246,6 +246,54 @@ bool planPrograms(const FirPeriodic& f, bool f64, int mp, BgPlan& plan) {
 }
 }  // namespace
 
+// Row-block-aligned programs (f64 plans): row block rb is cut into p = ceil(steps / kBgRbMaxSteps)
+// balanced K pieces, one program (one segment) each, finished by an LDS reduction in program order
+// when p > 1.  The persistent kernel runs them like any plan; bg_rb_kernel runs one (column block,
+// row block) per workgroup for small launches -- same programs, same sums.
+bool planProgramsRb(const FirPeriodic& f, bool f64, int mp, BgPlan& plan) {
+    double eff;
+    const std::vector<RbGeom> rbs = geomFor(f, mp, eff);
+    plan = BgPlan();
+    plan.f64 = f64;
+    plan.P = f.P; plan.Q = f.Q; plan.mp = mp;
+    plan.Pc = f.P * mp;
+    plan.Qc = f.Q * mp;
+    plan.nrb = static_cast<int>(rbs.size());
+    plan.rbAligned = true;
+    int maxLen = 0;
+    for (size_t rb = 0; rb < rbs.size(); ++rb) {
+        plan.Kc = std::max(plan.Kc, rbs[rb].klo + 4 * rbs[rb].nsteps);
+        const int n = rbs[rb].nsteps;
+        const int np = std::max(1, (n + kBgRbMaxSteps - 1) / kBgRbMaxSteps);
+        if (np > kBgRbMaxWaves || np > kBgMaxRedSlots) return false;
+        plan.rbStart.push_back(static_cast<int>(plan.progs.size()));
+        BgRed red;
+        red.rb = static_cast<int>(rb);
+        for (int i = 0, pos = 0; i < np; ++i) {
+            const int len = (n - pos + (np - i) - 1) / (np - i);  // balanced pieces, in K order
+            BgProg pg;
+            pg.nseg = 1;
+            pg.len = len;
+            pg.seg[0].rb = static_cast<int>(rb);
+            pg.seg[0].k0 = rbs[rb].klo + 4 * pos;
+            pg.seg[0].ns = len;
+            pg.seg[0].start = 0;
+            pg.seg[0].slot = np > 1 ? plan.nslots++ : -1;
+            if (np > 1) red.slot[red.n++] = pg.seg[0].slot;
+            plan.progs.push_back(pg);
+            maxLen = std::max(maxLen, len);
+            pos += len;
+        }
+        if (np > 1) plan.reds.push_back(red);
+    }
+    plan.rbStart.push_back(static_cast<int>(plan.progs.size()));
+    plan.kch = 1;
+    plan.NS = std::max(8, (maxLen + 3) / 4 * 4);
+    plan.ncg = 1;
+    plan.nw = std::min<int>(static_cast<int>(plan.progs.size()), std::min(16, bgMaxThreads(f64, plan.NS) / 64));
+    return true;
+}
+
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     if (f.P <= 0 || f.Q <= 0) return false;
     // Macro period (multiple of the FIR period) with the best useful/executed MAC ratio among
@@ -264,8 +312,11 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     std::stable_sort(cand.begin(), cand.end(),
                      [](const std::pair<double, int>& a, const std::pair<double, int>& b) { return a.first < b.first - 1e-9; });
     bool ok = false;
+    // f64: row-block-aligned programs where every row block fits kBgRbMaxWaves pieces (small
+    // launches then run bg_rb_kernel); longer filters (e.g. an 8191-tap decimator) the general split
     for (const auto& c : cand)
-        if ((ok = planPrograms(f, f64, c.second, plan))) break;
+        if (f64 && (ok = planProgramsRb(f, f64, c.second, plan))) break;
+    for (size_t i = 0; !ok && i < cand.size(); ++i) ok = planPrograms(f, f64, cand[i].second, plan);
     if (!ok) return false;
 
     const size_t np = plan.progs.size();

@@ -71,6 +71,11 @@ struct BgPlan {
     int nslots = 0;                   // LDS partial slots per column group
     std::vector<BgProg> progs;        // [nw]
     std::vector<BgRed> reds;          // row blocks finished by reduction
+    // Row-block-aligned plans (f64): every program is one K piece of one row block, so a workgroup
+    // can own one (column block, row block) pair -- the small-launch grid (bg_rb_kernel) -- and
+    // produce the same sums as the persistent kernel.  rbStart[rb] .. rbStart[rb + 1] = its programs.
+    bool rbAligned = false;
+    std::vector<int> rbStart;
     std::vector<float> A32;           // [nw][kch*NS][64] MFMA A fragments
     std::vector<double> A64;
     double usefulMacsPerOutput = 0;   // sum of row lengths / P
@@ -78,6 +83,9 @@ struct BgPlan {
     std::vector<int> progTable() const;  // [nprog][kBgProgInts]
     std::vector<int> redTable() const;   // [nred][kBgRedInts]
 };
+
+constexpr int kBgRbMaxSteps = 40;   // row-block-aligned plans: K steps per program (f64 MFMA: 40 x 64 cycles)
+constexpr int kBgRbMaxWaves = 8;    // ... and programs per row block (bg_rb_kernel workgroup <= 512 threads)
 
 // Builds the MFMA plan (macro period, balanced wave programs, A image).
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
