@@ -492,7 +492,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
 // element i of the new history is copied by thread i (mod the grid) of the flattened grid, issued right after the program's A / B loads so its memory round trip overlaps theirs.
 template <class TC>
 __device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g) {
-    if (g.hn <= 0) return;
+    if (g.hn <= 0 || (g.dbg & 64)) return;
     const int64_t total = g.hn * g.C;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -522,13 +522,13 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
             const ProgU pu = progLoad(p.progs + kBgProgInts * pr);
             TC A[NS], B[NS];
 #pragma unroll
-            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+            for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
             // rows of this lane: t0 + 4 s, s < NS (the zero-A tail steps read finite rows too)
             const int64_t t0 = a * g.Qc + pu.k0 + (lane >> 4);
             const int64_t lo = a * g.Qc + pu.k0, hi = lo + 4 * NS;
             const TC* dp = nullptr;
             int64_t ds = 0;
-            if (colOk && hi <= src.valid_end && lo >= 0) {
+            if (colOk && hi <= src.valid_end && lo >= 0 && !(g.dbg & (128 | 256))) {
                 if (srcSameType<TC>(src) && src.in && lo >= src.in_base && hi <= src.in_base + src.in_len) {
                     dp = static_cast<const TC*>(src.in) + (t0 - src.in_base) * src.in_fs + static_cast<int64_t>(c) * src.in_cs;
                     ds = 4 * src.in_fs;
@@ -537,14 +537,25 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
                     ds = 4 * src.hist_ld;
                 }
             }
-            if (dp) {
+            if (g.dbg & 16) {  // development (GAR_BG_DBG): no B loads
+#pragma unroll
+                for (int s = 0; s < NS; ++s) B[s] = TC(s);
+            } else if (dp) {
 #pragma unroll
                 for (int s = 0; s < NS; ++s) B[s] = dp[s * ds];
+            } else if (srcSameType<TC>(src) && !(g.dbg & 256)) {
+                // window across the history seam / past the input: branch-free gathers, so the NS
+                // loads issue together (a branchy srcRead per step waits out each round trip)
+#pragma unroll
+                for (int s = 0; s < NS; ++s) B[s] = srcReadBF<TC>(src, t0 + 4 * s, c, colOk, Aimg);
             } else {
 #pragma unroll
                 for (int s = 0; s < NS; ++s) B[s] = colOk ? srcRead<TC>(src, t0 + 4 * s, c) : TC(0);
             }
             if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside A / B's
+            // every A / B load issued before the first MFMA: one memory round trip for the program
+            // (left alone, the scheduler interleaves load -> wait -> MFMA, NS round trips deep)
+            __builtin_amdgcn_sched_barrier(0);
             V acc0 = {0, 0, 0, 0}, acc1 = acc0;
 #pragma unroll
             for (int s = 0; s < NS; ++s) {

@@ -14,7 +14,8 @@ y = torch.empty((int(chunk * nchunks * orr / ir) + 64 * (nchunks + 1), C), dtype
 def run():
     r.Reset(); o = 0
     for i in range(nchunks):
-        o += r.process_device(x[i * chunk:(i + 1) * chunk], out=y[o:]).shape[0]
+        j = 0 if os.environ.get("P_REUSE") else i  # P_REUSE: every call reads the same chunk (cache / TLB warm)
+        o += r.process_device(x[j * chunk:(j + 1) * chunk], out=y[o:]).shape[0]
     return o
 run(); torch.cuda.synchronize()
 r.profile(True)
