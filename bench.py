@@ -383,7 +383,10 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
             import torch.distributed as dist
             dist.barrier()
 
-    inline_prof = os.environ.get("GAR_BENCH_PROF_INLINE", "1") == "1" and not dry
+    # Kernel timing: HIP events around every launch, inside the timed region for one-launch steps
+    # (they agree with rocprof there); chunked workloads (hundreds of launches per step) take them in
+    # a separate pass after the timed steps, so the timed steps carry no event packets.
+    inline_prof = os.environ.get("GAR_BENCH_PROF_INLINE", "0" if w["chunk"] else "1") == "1" and not dry
     for _ in range(warmup):
         step()
     sync()
@@ -399,7 +402,7 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
     sync()
     barrier()
     t1 = time.perf_counter()
-    if not dry and not inline_prof:  # development: a separate profiled pass (the timed steps carry no event packets)
+    if not dry and not inline_prof:  # a separate profiled pass (the timed steps carry no event packets)
         r.profile(True)
         for k in range(6):
             r.profile_read(k)
@@ -452,6 +455,8 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
     if not dry:
         roof, kernel_keys = roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail)
         obj["roofline"] = roof
+        roof["kernel_timing"] = ("HIP events around each launch, inside the timed region" if inline_prof
+                                 else "HIP events around each launch, in a separate pass after the timed steps")
         obj["arith"] = (("int16 PCM I/O converted in the kernel's loads (float64(i)/32767 -> f32) and stores "
                          "(clamp, x32767, truncate); rms_vs_oracle in full-scale units includes the output "
                          "quantization (~0.6 LSB = 1.8e-5); " if pcm_scale else "f32 I/O; ") +
