@@ -202,6 +202,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.fastHi = rawOk ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
     x.fmt = fmt;
     x.small = small ? 1 : 0;
+    static const int knobSmallK = std::getenv("GAR_HXS_SMALLK") ? std::atoi(std::getenv("GAR_HXS_SMALLK")) : 1;
+    x.bigSmall = knobSmallK ? 0 : 1;
     static const int knobNt = std::getenv("GAR_HXS_NT") ? std::atoi(std::getenv("GAR_HXS_NT")) : 0;
     static const int knobPair = std::getenv("GAR_HXS_PAIR") ? std::atoi(std::getenv("GAR_HXS_PAIR")) : 1;
     x.nt = knobNt;

@@ -73,6 +73,7 @@ struct HxsArgs {
     int dbg;               // development attribution (GAR_HXS_DBG, wrong output): 1 no steady DMAs, 2 no stores,
                            // 4 no MFMA, 16 no steady conversion
     int small;             // one period per column, window staged in one pass (hxsSmallStage)
+    int bigSmall;          // development (GAR_HXS_SMALLK=0): small launches on hxs_kernel instead of hxs_small_kernel
     int vst, fmt;          // epilogue layout (template VST), load layout 0 gathered / 1 STEREO / 2 ROW16
     int xcdPair;           // ROW16 blocks 2m, 2m+1 share every 128-B input/output line: run them on one XCD
     int nt;                // development: non-temporal output stores (GAR_HXS_NT)
@@ -320,16 +321,28 @@ __device__ __forceinline__ void hxsSmallStage(XP x, int b, int tid, int nth, cha
     st.T0 = 0;
     st.nrow = x->Wg;
     st.fast = false;
-    for (int i = tid; i < 4 * x->Wg; i += nth) {
-        const int q = i & 3, row = i >> 2;
-        f32x4 e;
+    // batches of kB items per thread: every gather of a batch issues before the first conversion,
+    // so the window costs one memory round trip per batch, not one per item
+    constexpr int kB = 4;
+    const int nit = 4 * x->Wg;
+    for (int i0 = tid; i0 < nit; i0 += kB * nth) {
+        f32x4 e[kB];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
-            const int col = b * 16 + 4 * q + n;
-            const int k = col / x->C, c = col - k * x->C;
-            e[n] = col < x->ncols ? hxsGather(src, hxsChunkRow(x, k, row), c, x->A) : 0.f;
+        for (int u = 0; u < kB; ++u) {
+            const int i = i0 + u * nth;
+            const int q = i & 3, row = i >> 2;
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                const int col = b * 16 + 4 * q + n;
+                const int k = col / x->C, c = col - k * x->C;
+                e[u][n] = (i < nit && col < x->ncols) ? hxsGather(src, hxsChunkRow(x, k, row), c, x->A) : 0.f;
+            }
         }
-        hxsPutItem(x, st, 0, q, row, e, ring, QS, loudLo, loudHi, flag);
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int i = i0 + u * nth;
+            if (i < nit) hxsPutItem(x, st, 0, i & 3, i >> 2, e[u], ring, QS, loudLo, loudHi, flag);
+        }
     }
 }
 
@@ -834,8 +847,100 @@ __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
 }
 
 // Launch (explicitly instantiated in gar_hxs_i*.hip).
+// Small launches (x.small: stream chunks, flush tails -- one macro period per column): a compact
+// kernel of compute waves only, so the launch runs a short, warm instruction stream instead of the
+// streaming kernel's loader / ring / format machinery (whose cold code dominated a 4096-frame call).
+// Same window image, same A fragments, same MFMA order and epilogue as hxs_kernel: identical bits.
+//   all waves: gather the block's window [0, Wg) into the image (hxsSmallStage) | barrier |
+//   wave w < nprog: row block w, NS steps of 3 MFMAs, scale, store | loud fixup | history keep.
+template <int NS, int VST>
+__global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;
+    char* ring = reinterpret_cast<char*>(smem);
+    int* loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(QS));
+    int* loudHi = loudLo + 16;
+    int* flag = loudHi + 16;
+    const int lane = threadIdx.x & 63;
+    const int wt = uni(threadIdx.x >> 6);
+    const int grp = lane >> 4, l16 = lane & 15;
+    const bool comp = wt < x.nprog;
+    h8v Ah[NS], Al[NS];
+    int u0 = 0, rbw = 0;
+    if (comp) {  // A lands while the window is gathered
+        const int* pt = x.progs + kBgProgInts * wt;
+        u0 = uni(pt[4]);
+        rbw = uni(pt[3]);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
+            Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
+        }
+    }
+    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+    const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
+    const int sh = -(x.ea + kHxXs);
+    for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
+        if (threadIdx.x < 16) { loudLo[threadIdx.x] = INT_MAX; loudHi[threadIdx.x] = -1; }
+        if (threadIdx.x == 0) *flag = 0;
+        __syncthreads();  // loud state reset; the previous block's image reads done
+        hxsSmallStage(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag);
+        __syncthreads();  // the whole window in the image
+        if (comp) {
+            const uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) + 8u * static_cast<uint32_t>(u0);
+            f32x4 nA = {0, 0, 0, 0}, nL = nA;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const h8v bh = bFragA(aH + 256 * s), bl = bFragA(aH + dL + 256 * s);
+                nA = mfma16(Ah[s], bh, nA);
+                nA = mfma16(Al[s], bh, nA);
+                nL = mfma16(Ah[s], bl, nL);
+            }
+            const f32x4 y = hxScale(nA, nL, sh);
+            const int col = b * 16 + l16;
+            const bool colOk = col < x.ncols;
+            const int kcol = col / x.C, ccol = col - kcol * x.C;
+            const int64_t a = x.a_lo + static_cast<int64_t>(kcol) * x.Np;  // Np == 1: the column's one period
+            const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;
+            const int64_t o0 = a * x.Pc + oRow0;
+            const bool fullRb = (rbw + 1) * 16 <= x.Pc;
+            const bool live = colOk && a < x.a_hi;
+            // whole-period stores need both lanes of a stereo pair (same chunk: same condition)
+            if (fullRb && live && (!x.out_pcm || VST == 4) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+                char* pp = x.out + (o0 + (((VST == 2 || VST == 4) && (lane & 1)) ? 2 : 0)) * x.out_fs +
+                           ((VST == 2 || VST == 4) ? 0 : ccol * x.out_cs);
+                hxsStoreFast<VST>(x, pp, y, lane);
+            } else if (live) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t o = o0 + i;
+                    if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi) {
+                        char* pp = x.out + o * x.out_fs + ccol * x.out_cs;
+                        if (x.out_pcm) pcmWrite(pp, 0, x.out_pcm, static_cast<double>(y[i]));
+                        else if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
+                        else *reinterpret_cast<float*>(pp) = y[i];
+                    }
+                }
+            }
+        }
+        if (*flag) {  // uniform (LDS after the barrier)
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            hxsFixup(hxsCold(), b, loudLo, loudHi);
+        }
+        __syncthreads();  // every wave done with the image / loud state before the next block
+    }
+    if (x.hn > 0) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+                              static_cast<int64_t>(gridDim.x) * blockDim.x);
+}
+
 template <int NS, int VST>
 hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    if (x.small && !x.bigSmall) {
+        setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>));
+        hipLaunchKernelGGL((hxs_small_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * x.nprog), lds, st, x);
+        return hipGetLastError();
+    }
     setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>));
     hipLaunchKernelGGL((hxs_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.nprog + kHxsLoaders)), lds, st, x);
     return hipGetLastError();
