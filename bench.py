@@ -567,8 +567,9 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
         roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
-        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel"]
-        kname = (f"{'poly_kernel<double>' if dom == 4 else 'bg_kernel<double>'} ({KIND_NAMES[dom]}, stage {sidx}: "
+        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel", "bg_rb_kernel"]
+        chunked = bool(w["chunk"])
+        kname = (f"{'poly_kernel<double>' if dom == 4 else ('bg_rb_kernel<double>' if chunked else 'bg_kernel<double>')} ({KIND_NAMES[dom]}, stage {sidx}: "
                  f"{48000:g}->{48000 * st_ratio:g} Hz engine, v_mfma_f64_16x16x4_f64)")
         algo_unit_bytes = (st_in + st_out) * 8 / per_step
         roof["useful_macs_per_output"] = round(st_geom.useful_macs_per_output, 2)

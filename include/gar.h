@@ -45,7 +45,11 @@ enum { GAR_QUALITY_QUICK = 0, GAR_QUALITY_LOW = 1, GAR_QUALITY_MEDIUM = 2, GAR_Q
 enum { GAR_FLAG_NO_INTERPOLATION = 1, GAR_FLAG_MINIMUM_PHASE = 2, GAR_FLAG_LINEAR_PHASE = 4,
        GAR_FLAG_ALLOW_ALIASING = 8, GAR_FLAG_NO_SIMD = 16 };
 /* sample / compute types.  Compute: GAR_F64 (the reference's float64), GAR_F32 (float32-class:
- * f16-split products on the f16 matrix cores, f32 accumulation, error <= exact-f32 arithmetic's),
+ * f16-split products on the f16 matrix cores, f32 accumulation, error <= exact-f32 arithmetic's
+ * for full-scale material; the fixed input split scale 2^12 gives inputs an ABSOLUTE precision
+ * floor of about 2^-47 (f16 subnormals), so material quieter than ~2^-26 (-156 dBFS) loses the
+ * relative precision the reference's float64 New path keeps -- choose GAR_F64 or GAR_F32_EXACT
+ * for such signals; |x| >= 16, Inf and NaN are recomputed exactly in f64),
  * GAR_F32_EXACT (exact f32 products on the f32 matrix cores). */
 enum { GAR_F64 = 0, GAR_F32 = 1, GAR_F32_EXACT = 2 };
 /* integer PCM sample types of the device entry points (in_dtype / out_dtype of gar_process_device
