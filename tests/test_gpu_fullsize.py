@@ -75,6 +75,34 @@ def test_cfg3_full_256ch_10s(gar, O, cuda):
     np.testing.assert_array_equal(s[:, 0], y[:, 101].cpu().numpy())
 
 
+def test_northstar_256ch_44k1_48k_60s(gar, O, cuda):
+    """north_star workload: 256-channel float32 44.1k->48k QualityHigh, 60 s, one Process + Flush
+    (the ROW16 streaming kernel): exact length, a channel subset vs the oracle over the whole
+    stream, the reference's 4096-frame ProcessInto pattern == one shot bit for bit (small-launch
+    kernel vs streaming kernel), and a channel resampled alone == its column of the 256."""
+    frames, ch = 2_646_000, 256
+    xd = synth_torch(cuda, frames, ch, 44100, 256)
+    r = gar.New(gar.Config(44100, 48000, ch, gar.QualityHigh, ComputeDtype=gar.F32))
+    y = cuda.cat([r.process_device(xd), r.flush_device()])
+    assert y.shape[0] == 2_880_002                  # 44100 -> 48000 over 60 s + the flush tail
+    x = xd[:, [0, 77, 255]].double().cpu().numpy()
+    yc = y[:, [0, 77, 255]].double().cpu().numpy()
+    for j in range(3):
+        want = oracle_new(O, 44100, 48000, x[:, j:j + 1], O.P_HIGH)[0]
+        assert len(want) == y.shape[0]
+        assert rms(yc[:, j], want) <= F32_RMS_TOL
+    m = 44100 * 5
+    r.Reset()
+    one = cuda.cat([r.process_device(xd[:m]), r.flush_device()]).cpu().numpy()
+    r.Reset()
+    outs = [r.process_device(xd[s:s + n]).clone() for s, n in zip(range(0, m, 4096), chunk_sizes(m, 4096))]
+    outs.append(r.flush_device())
+    np.testing.assert_array_equal(cuda.cat(outs).cpu().numpy(), one)
+    solo = gar.New(gar.Config(44100, 48000, 1, gar.QualityHigh, ComputeDtype=gar.F32))
+    s = cuda.cat([solo.process_device(xd[:, 77:78].contiguous()), solo.flush_device()]).cpu().numpy()
+    np.testing.assert_array_equal(s[:, 0], y[:, 77].cpu().numpy())
+
+
 def test_cfg4_full_1024_stereo_streams(gar, O, cuda):
     streams, frames = 1024, 441_000
     xd = synth_torch(cuda, frames, 2 * streams, 44100, 4)
