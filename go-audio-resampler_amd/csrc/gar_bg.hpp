@@ -75,6 +75,10 @@ struct BgGrid {
     int dbg;  // development timing knob (GAR_BG_DBG): 1 skip tile DMA after the first, 2 skip stores
     int vst;  // f32 epilogue: 0 scalar, 1 channel-contiguous (fs == 1), 2 stereo interleaved (C == 2, fs == 2, cs == 1)
     int rbMode;  // small launch of a row-block-aligned plan: bg_rb_kernel (G = 1)
+    // bg_rb_kernel: program ranges and first input rows passed by value (kernarg), so a wave issues
+    // its A and B loads without first loading its program from the tables
+    int rbStart[kBgRbKMaxRb + 1];
+    int rbK0[kBgRbKMaxProg];
     void* hdst;       // folded history keep (HistCopy): hdst[(t - ht0) * C + c] = src(t, c), t < ht0 + hn
     int64_t ht0, hn;
 };
@@ -511,7 +515,7 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
     const int nv = g.nblocks * p.nrb;
     for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
         const int b = v / p.nrb, rb = v - b * p.nrb;
-        const int ps = p.rbStart[rb], np = p.rbStart[rb + 1] - ps;
+        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
         const int col = b * 16 + (lane & 15);
         const bool colOk = col < g.ncols;
         const int c = colOk ? col % g.C : 0;
@@ -519,13 +523,13 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
         V r = {0, 0, 0, 0};
         if (wt < np) {
             const int pr = ps + wt;
-            const ProgU pu = progLoad(p.progs + kBgProgInts * pr);
+            const int k0 = g.rbK0[pr];
             TC A[NS], B[NS];
 #pragma unroll
             for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
             // rows of this lane: t0 + 4 s, s < NS (the zero-A tail steps read finite rows too)
-            const int64_t t0 = a * g.Qc + pu.k0 + (lane >> 4);
-            const int64_t lo = a * g.Qc + pu.k0, hi = lo + 4 * NS;
+            const int64_t t0 = a * g.Qc + k0 + (lane >> 4);
+            const int64_t lo = a * g.Qc + k0, hi = lo + 4 * NS;
             const TC* dp = nullptr;
             int64_t ds = 0;
             if (colOk && hi <= src.valid_end && lo >= 0 && !(g.dbg & (128 | 256))) {
@@ -578,7 +582,7 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
         }
     }
     const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;  // the first (column block, row block) of this workgroup
-    if (wt >= p.rbStart[rb0 + 1] - p.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
+    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
 }
 
 template <class TC, int NS>

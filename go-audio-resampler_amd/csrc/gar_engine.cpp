@@ -164,6 +164,8 @@ BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
     d.nred = static_cast<int>(p.reds.size());
     d.nslots = p.nslots;
     d.rbAligned = p.rbAligned ? 1 : 0;
+    d.hRbStart = p.rbAligned ? p.rbStart.data() : nullptr;  // the plan lives as long as the stage
+    d.hRbK0 = p.rbAligned ? p.rbK0.data() : nullptr;
     for (size_t rb = 0; p.rbAligned && rb + 1 < p.rbStart.size(); ++rb)
         d.maxPrb = std::max(d.maxPrb, p.rbStart[rb + 1] - p.rbStart[rb]);
     if (dry) return d;

@@ -69,8 +69,11 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     // small launch of a row-block-aligned f64 plan (stream chunks): one (column block, row block) per
     // workgroup, one macro period per column (bg_rb_kernel) -- same programs, same sums
-    if (p.f64 && p.rbAligned && p.rbStart && (nmac * C + 15) / 16 <= 2 * static_cast<int64_t>(ncu) && !(knobDbg & 8)) {
+    if (p.f64 && p.rbAligned && p.rbStart && p.hRbStart && p.nrb <= kBgRbKMaxRb && p.nprog <= kBgRbKMaxProg &&
+        (nmac * C + 15) / 16 <= 2 * static_cast<int64_t>(ncu) && !(knobDbg & 8)) {
         g.rbMode = 1;
+        for (int i = 0; i <= p.nrb; ++i) g.rbStart[i] = p.hRbStart[i];
+        for (int i = 0; i < p.nprog; ++i) g.rbK0[i] = p.hRbK0[i];
         g.G = 1;
         g.W = p.Kc;
         g.Wl = p.Kread;

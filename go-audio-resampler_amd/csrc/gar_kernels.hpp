@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace gar {
 
@@ -62,6 +63,8 @@ struct BgDev {
     int rbAligned;      // BgPlan::rbAligned: small launches may run bg_rb_kernel
     int maxPrb;         // most programs of one row block
     const int* rbStart; // [nrb + 1]
+    const int* hRbStart; // host copies (bg_rb_kernel passes them by value): [nrb + 1]
+    const int* hRbK0;    // first input row of each program [nprog]
 };
 
 // Device copy of an HxPlan (gar_plan.hpp): split-f16 MFMA FIR, f32 compute.

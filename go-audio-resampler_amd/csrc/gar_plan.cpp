@@ -281,6 +281,7 @@ bool planProgramsRb(const FirPeriodic& f, bool f64, int mp, BgPlan& plan) {
             pg.seg[0].slot = np > 1 ? plan.nslots++ : -1;
             if (np > 1) red.slot[red.n++] = pg.seg[0].slot;
             plan.progs.push_back(pg);
+            plan.rbK0.push_back(pg.seg[0].k0);
             maxLen = std::max(maxLen, len);
             pos += len;
         }

@@ -76,6 +76,7 @@ struct BgPlan {
     // produce the same sums as the persistent kernel.  rbStart[rb] .. rbStart[rb + 1] = its programs.
     bool rbAligned = false;
     std::vector<int> rbStart;
+    std::vector<int> rbK0;            // first input row of each program (one segment each)
     std::vector<float> A32;           // [nw][kch*NS][64] MFMA A fragments
     std::vector<double> A64;
     double usefulMacsPerOutput = 0;   // sum of row lengths / P
@@ -86,6 +87,8 @@ struct BgPlan {
 
 constexpr int kBgRbMaxSteps = 40;   // row-block-aligned plans: K steps per program (f64 MFMA: 40 x 64 cycles)
 constexpr int kBgRbMaxWaves = 8;    // ... and programs per row block (bg_rb_kernel workgroup <= 512 threads)
+constexpr int kBgRbKMaxRb = 24;     // bg_rb_kernel launches: row blocks / programs whose tables fit the kernel
+constexpr int kBgRbKMaxProg = 96;   // arguments (BgGrid::rbStart, rbK0)
 
 // Builds the MFMA plan (macro period, balanced wave programs, A image).
 bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan);
