@@ -313,10 +313,64 @@ int64_t cntDecim(Counters& s, const DecimBank& b, int64_t n) {
     return nout;
 }
 
+// Exact closed form of the CubicStage phase walk.  In units of 2^-F (F = 53 - exponent of step,
+// so step = S units exactly) every value the walk forms -- ph, ph + k*step < 1, the first sum >= 1,
+// that sum minus 1 -- is an integer.  When S, the start phase P0 and 2^F are all multiples of the
+// rounding grid of the largest binade a sum reaches (sums < 1 + step), no float64 addition of the
+// walk rounds (the "- 1" never does: Sterbenz), so the walk is the exact rotation
+//     P_{i+1} = P_i + n_i*S - 2^F in [0, S)   =>   P_i = (P0 - i*2^F) mod S,
+//     outputs before input i: N_i = (i*2^F + P_i - P0) / S,
+// the same phases and counts as the sequential loop, in O(1) per checkpoint (e.g. 44.1k->48k:
+// S even, grid 2 units).  Ratios whose step has a low set bit on a coarser grid (48k->44.1k) walk.
+namespace {
+struct CubicRot {
+    int F = 0;
+    int64_t S = 0, P0 = 0;
+};
+bool cubicRotation(double step, double ph, CubicRot& r) {
+    int e = 0;
+    (void)std::frexp(step, &e);  // step = m * 2^e, m in [0.5, 1)
+    r.F = 53 - e;
+    if (r.F < 1 || r.F > 60) return false;
+    const double Sd = std::ldexp(step, r.F), Pd = std::ldexp(ph, r.F);  // exact (powers of two)
+    if (Sd != std::floor(Sd) || Pd != std::floor(Pd) || Pd < 0.0 || Pd >= Sd) return false;
+    r.S = static_cast<int64_t>(Sd);
+    r.P0 = static_cast<int64_t>(Pd);
+    const int64_t one = int64_t(1) << r.F;
+    // bits of the largest sum (< one + S): its binade's grid is 2^(bits - 53) units
+    int bits = 0;
+    for (uint64_t v = static_cast<uint64_t>(one + r.S - 1); v; v >>= 1) ++bits;
+    const int64_t grid = bits > 53 ? (int64_t(1) << (bits - 53)) : 1;
+    return r.S % grid == 0 && r.P0 % grid == 0 && one % grid == 0;
+}
+}  // namespace
+
 // CubicStage.Process walk (cubic.go:42-61): the f64 phase recurrence, run once for
 // all channels; `segs` (when given) receives the state every kCubicSegInputs inputs.
 int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* segs) {
     const double step = 1.0 / ratio;
+    CubicRot rot;
+    if (n > 0 && cubicRotation(step, s.cub_phase, rot)) {
+        const __int128 one = static_cast<__int128>(1) << rot.F, S = rot.S, P0 = rot.P0;
+        auto phaseAt = [&](int64_t i) {  // P_i in [0, S)
+            __int128 v = (P0 - static_cast<__int128>(i) * one) % S;
+            return v < 0 ? v + S : v;
+        };
+        auto outsBefore = [&](int64_t i, __int128 Pi) {
+            return static_cast<int64_t>((static_cast<__int128>(i) * one + Pi - P0) / S);
+        };
+        if (segs)
+            for (int64_t i = 0; i < n; i += kCubicSegInputs) {
+                const __int128 Pi = phaseAt(i);
+                segs->push_back({std::ldexp(static_cast<double>(static_cast<int64_t>(Pi)), -rot.F), s.y_count + outsBefore(i, Pi),
+                                 s.x_count + i});
+            }
+        const __int128 Pn = phaseAt(n);
+        const int64_t nout = outsBefore(n, Pn);
+        s.cub_phase = std::ldexp(static_cast<double>(static_cast<int64_t>(Pn)), -rot.F);
+        s.x_count += n;
+        return nout;
+    }
     double ph = s.cub_phase;
     int64_t nout = 0;
     for (int64_t i = 0; i < n; ++i) {

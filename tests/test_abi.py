@@ -332,3 +332,21 @@ def test_stage_geometry_matches_oracle_pipeline(gar, O, i, o, preset):
             assert (g.poly_phases, g.poly_taps, g.poly_step) == (s.poly_phases, s.poly_taps_per_phase, s.poly_step)
         if s.decim_factor:
             assert (g.decim_factor, g.decim_taps) == (s.decim_factor, s.decim_taps)
+
+
+@pytest.mark.parametrize("i,o", [(44100, 48000), (96000, 8000), (44100, 44100), (48000, 96000), (48000, 44100)])
+def test_quick_phase_walk_long_stream(gar, O, i, o):
+    """QualityQuick phase walk over a long stream in ragged calls: every call's output count equals the
+    reference's sequential float64 walk (cubic.go:42-61).  44.1k->48k, 96k->8k, 1:1 and 2x take the
+    exact closed form (cntCubic: every f64 addition of the walk is exact there); 48k->44.1k walks."""
+    rng = np.random.default_rng(7)
+    e = O.Engine(i, o, O.lib().o_preset_to_engine_quality(0))
+    r = gar.NewEngineDry(i, o, 0)
+    total = 0
+    while total < 3_000_000:
+        n = int(rng.choice([1, 3, 4095, 4096, 65536, 250_000, 1_000_003]))
+        x = np.zeros(n)
+        assert r.OutputSize(n) == len(e.process(x)), (total, n)
+        r.Process(x)
+        total += n
+    assert r.FlushSize() == len(e.flush())
