@@ -346,8 +346,9 @@ bool cubicRotation(double step, double ph, CubicRot& r) {
 }  // namespace
 
 // CubicStage.Process walk (cubic.go:42-61): the f64 phase recurrence, run once for
-// all channels; `segs` (when given) receives the state every kCubicSegInputs inputs.
-int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* segs) {
+// all channels; `segs` (when given) receives the state every segLen inputs (the closed form takes the
+// caller's spacing -- short segments for short calls; the sequential walk uses kCubicSegInputs).
+int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* segs, int* segLen = nullptr) {
     const double step = 1.0 / ratio;
     CubicRot rot;
     if (n > 0 && cubicRotation(step, s.cub_phase, rot)) {
@@ -360,7 +361,7 @@ int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* se
             return static_cast<int64_t>((static_cast<__int128>(i) * one + Pi - P0) / S);
         };
         if (segs)
-            for (int64_t i = 0; i < n; i += kCubicSegInputs) {
+            for (int64_t i = 0; i < n; i += (segLen ? *segLen : kCubicSegInputs)) {
                 const __int128 Pi = phaseAt(i);
                 segs->push_back({std::ldexp(static_cast<double>(static_cast<int64_t>(Pi)), -rot.F), s.y_count + outsBefore(i, Pi),
                                  s.x_count + i});
@@ -371,6 +372,7 @@ int64_t cntCubic(Counters& s, double ratio, int64_t n, std::vector<CubicSeg>* se
         s.x_count += n;
         return nout;
     }
+    if (segLen) *segLen = static_cast<int>(kCubicSegInputs);
     double ph = s.cub_phase;
     int64_t nout = 0;
     for (int64_t i = 0; i < n; ++i) {
@@ -776,7 +778,10 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             if (segs) segs->clear();
             const SrcDesc src = mkSrc(dv.xh, C, x0, in);
             const int64_t y0 = c.y_count;
-            const int64_t nout = cntCubic(c, d.ratio, n, segs);
+            // short calls (streaming chunks): short segments, so each GPU thread re-walks only a few
+            // inputs from registers (a 4096-frame call would otherwise be 16 serial 256-input walks)
+            int segLen = n * C <= (int64_t(1) << 20) ? kCubicSegInputsShort : static_cast<int>(kCubicSegInputs);
+            const int64_t nout = cntCubic(c, d.ratio, n, segs, &segLen);
             if (x.launch && nout > 0) {
                 PinBuf& pb = x.g->cubPin[x.g->cubCur];
                 x.g->cubCur ^= 1;
@@ -784,7 +789,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                 std::memcpy(hp, segs->data(), segs->size() * sizeof(CubicSeg));
                 HIPCHK(timed(x, 5, [&] {
                     return launchCubic(rt.f64 ? 1 : 0, static_cast<const CubicSeg*>(hp), static_cast<int64_t>(segs->size()),
-                                       c.x_count, 1.0 / d.ratio, src, mkOut(out, y0, nout), C, x.s);
+                                       c.x_count, 1.0 / d.ratio, src, mkOut(out, y0, nout), C, x.s, segLen);
                 }));
                 pb.issued(x.s);
             }

@@ -380,9 +380,20 @@ hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& od, i
 // inputs; one thread per (segment, channel) re-walks its segment with the same
 // f64 operations, so every output sits at the reference's phase bit for bit.
 // ---------------------------------------------------------------------------
-template <class TC>
+// The cubic output of phase ph between h2 (s[0]) and h1 (s[1]) (cubic.go:78-89; contraction off).
+__device__ __forceinline__ double cubicAt(double h3, double h2, double h1, double h0, double ph) {
+#pragma clang fp contract(off)
+    const double b = 0.5 * (h1 + h3) - h2;
+    const double a = (1.0 / 6.0) * (h0 - h1 + h3 - h2 - 4 * b);
+    const double cc = h1 - h2 - a - b;
+    return ((a * ph + b) * ph + cc) * ph + h2;
+}
+
+// SHORT: segments of kCubicSegInputsShort inputs (short calls) -- the segment's inputs and the three
+// before it are loaded up front (one memory round trip) and the walk runs from registers.
+template <class TC, bool SHORT>
 __global__ __launch_bounds__(256) void cubic_kernel(const CubicSeg* segs, int64_t nseg, int64_t x_end, double step,
-                                                    SrcDesc src, OutDesc od, int C) {
+                                                    SrcDesc src, OutDesc od, int C, int segLen) {
 #pragma clang fp contract(off)
     const int64_t total = nseg * C;
     for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; idx < total;
@@ -390,38 +401,61 @@ __global__ __launch_bounds__(256) void cubic_kernel(const CubicSeg* segs, int64_
         const int64_t sgi = idx / C;
         const int c = static_cast<int>(idx - sgi * C);
         const CubicSeg sg = segs[sgi];
-        const int64_t i1 = min(sg.i + kCubicSegInputs, x_end);
-        // history[3..1] = inputs i-3 .. i-1 (zeros before the stream start)
-        double h3 = static_cast<double>(srcRead<TC>(src, sg.i - 3, c));
-        double h2 = static_cast<double>(srcRead<TC>(src, sg.i - 2, c));
-        double h1 = static_cast<double>(srcRead<TC>(src, sg.i - 1, c));
+        const int64_t i1 = min(sg.i + segLen, x_end);
         double ph = sg.phase;
         int64_t o = sg.o;
-        for (int64_t i = sg.i; i < i1; ++i) {
-            const double h0 = static_cast<double>(srcRead<TC>(src, i, c));
-            while (ph < 1.0) {
-                // s[-1], s[0], s[1], s[2] = history[3], [2], [1], [0] (cubic.go:78-89)
-                const double b = 0.5 * (h1 + h3) - h2;
-                const double a = (1.0 / 6.0) * (h0 - h1 + h3 - h2 - 4 * b);
-                const double cc = h1 - h2 - a - b;
-                outWrite<TC>(od, o, c, static_cast<TC>(((a * ph + b) * ph + cc) * ph + h2));
-                ++o;
-                ph += step;
+        if constexpr (SHORT) {
+            constexpr int L = kCubicSegInputsShort;
+            double v[L + 3];
+#pragma unroll
+            for (int k = 0; k < L + 3; ++k)
+                v[k] = (sg.i - 3 + k < i1) ? static_cast<double>(srcRead<TC>(src, sg.i - 3 + k, c)) : 0.0;
+#pragma unroll
+            for (int k = 0; k < L; ++k) {
+                if (sg.i + k >= i1) break;
+                // history[3..1] = v[k], v[k+1], v[k+2]; the new input h0 = v[k+3]
+                while (ph < 1.0) {
+                    outWrite<TC>(od, o, c, static_cast<TC>(cubicAt(v[k], v[k + 1], v[k + 2], v[k + 3], ph)));
+                    ++o;
+                    ph += step;
+                }
+                ph -= 1.0;
             }
-            ph -= 1.0;
-            h3 = h2; h2 = h1; h1 = h0;
+        } else {
+            // history[3..1] = inputs i-3 .. i-1 (zeros before the stream start)
+            double h3 = static_cast<double>(srcRead<TC>(src, sg.i - 3, c));
+            double h2 = static_cast<double>(srcRead<TC>(src, sg.i - 2, c));
+            double h1 = static_cast<double>(srcRead<TC>(src, sg.i - 1, c));
+            for (int64_t i = sg.i; i < i1; ++i) {
+                const double h0 = static_cast<double>(srcRead<TC>(src, i, c));
+                while (ph < 1.0) {
+                    // s[-1], s[0], s[1], s[2] = history[3], [2], [1], [0] (cubic.go:78-89)
+                    outWrite<TC>(od, o, c, static_cast<TC>(cubicAt(h3, h2, h1, h0, ph)));
+                    ++o;
+                    ph += step;
+                }
+                ph -= 1.0;
+                h3 = h2; h2 = h1; h1 = h0;
+            }
         }
     }
 }
 
 hipError_t launchCubic(int f64, const CubicSeg* segs, int64_t nseg, int64_t x_end, double step, const SrcDesc& src,
-                       const OutDesc& od, int C, hipStream_t stream) {
+                       const OutDesc& od, int C, hipStream_t stream, int segLen) {
     if (nseg <= 0) return hipSuccess;
     const int64_t total = nseg * C;
     int64_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    if (f64) hipLaunchKernelGGL(cubic_kernel<double>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, segs, nseg, x_end, step, src, od, C);
-    else hipLaunchKernelGGL(cubic_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, segs, nseg, x_end, step, src, od, C);
+    const bool sh = segLen <= kCubicSegInputsShort;
+    const dim3 gd(static_cast<unsigned>(blocks)), bd(256);
+    if (f64) {
+        if (sh) hipLaunchKernelGGL((cubic_kernel<double, true>), gd, bd, 0, stream, segs, nseg, x_end, step, src, od, C, segLen);
+        else hipLaunchKernelGGL((cubic_kernel<double, false>), gd, bd, 0, stream, segs, nseg, x_end, step, src, od, C, segLen);
+    } else {
+        if (sh) hipLaunchKernelGGL((cubic_kernel<float, true>), gd, bd, 0, stream, segs, nseg, x_end, step, src, od, C, segLen);
+        else hipLaunchKernelGGL((cubic_kernel<float, false>), gd, bd, 0, stream, segs, nseg, x_end, step, src, od, C, segLen);
+    }
     return hipGetLastError();
 }
 

@@ -108,6 +108,7 @@ struct CubicSeg {
     int64_t o, i;
 };
 constexpr int64_t kCubicSegInputs = 256;
+constexpr int kCubicSegInputsShort = 16;  // segment of short calls (closed-form walks only)
 
 // Launchers (all asynchronous on `stream`).  Return hipSuccess or the launch error.
 // Optional history keep folded into a streaming FIR launch: dst[(t - t0) * C + c] = src(t, c) for
@@ -134,7 +135,7 @@ hipError_t launchPoly(const PolyDev& p, const SrcDesc& src, const OutDesc& out, 
 // CubicStage outputs of nseg checkpointed segments (segs readable by the device:
 // pinned host or device memory); x_end = one past the last input; step = 1/ratio.
 hipError_t launchCubic(int f64, const CubicSeg* segs, int64_t nseg, int64_t x_end, double step, const SrcDesc& src,
-                       const OutDesc& od, int C, hipStream_t stream);
+                       const OutDesc& od, int C, hipStream_t stream, int segLen = static_cast<int>(kCubicSegInputs));
 // dst[(t - t0) * C + c] = src(t, c) for t in [t0, t0 + n): history compaction / materialisation.
 hipError_t launchGather(int f64, const SrcDesc& src, void* dst, int64_t t0, int64_t n, int C, hipStream_t stream);
 // Strided copy with dtype conversion (pass-through stages, group split).
