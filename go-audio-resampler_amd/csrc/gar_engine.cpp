@@ -502,7 +502,10 @@ class Pool {
         return p;
     }
     void run(int n, const std::function<void(int)>& f) {
-        if (n <= 1 || th_.empty()) {
+        // one job at a time: handles are independent, so a second thread's call must not
+        // overwrite a running job; when the pool is busy that caller runs its job inline
+        std::unique_lock<std::mutex> owner(runMu_, std::try_to_lock);
+        if (n <= 1 || th_.empty() || !owner.owns_lock()) {
             for (int i = 0; i < n; ++i) f(i);
             return;
         }
@@ -557,6 +560,7 @@ class Pool {
         }
     }
     std::vector<std::thread> th_;
+    std::mutex runMu_;  // held by the caller whose job the workers run
     std::mutex mu_;
     std::condition_variable cv_, done_;
     const std::function<void(int)>* job_ = nullptr;
@@ -587,6 +591,9 @@ inline void forSlices(int C, int64_t n, size_t bytesPerSample, const std::functi
 struct Group {
     int c0 = 0, C = 1;
     std::vector<Counters> cnt;
+    // engine.Resampler.GetStatistics counters per channel (resampler.go:187-195,270,320,338-339):
+    // samples in per non-empty Process, samples out per Process and Flush, zeroed by Reset
+    int64_t statIn = 0, statOut = 0;
     std::vector<StageDev> dev;
     std::vector<DevBuf> tmp;   // per stage-boundary output buffers
     DevBuf utmp;               // staged DFT output (u) scratch
@@ -617,6 +624,7 @@ struct gar_resampler {
     // a HIP failure mid-call may leave counters advanced past the histories: refuse
     // further work until Reset (ADVICE: no silent wrong output)
     bool poisoned = false;
+    hipStream_t failStream = nullptr;  // the stream of the call that poisoned the handle
     gar_config cfg{};
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
@@ -637,6 +645,15 @@ namespace gar {
 namespace {
 
 using Handle = gar_resampler;
+
+// Pinned host staging above kPinKeep bytes is released when the call that grew it returns, so a
+// one-shot call on a long stream does not keep hundreds of MB of page-locked memory per handle.
+constexpr size_t kPinKeep = size_t(64) << 20;
+// Called only after the call's stream has been synchronised (no kernel still reads the buffers).
+void trimHost(Handle* h) {
+    if (h->hostIn.cap > kPinKeep) h->hostIn.release();
+    if (h->hostOut.cap > kPinKeep) h->hostOut.release();
+}
 
 struct Ctx {
     Handle* h;
@@ -1045,6 +1062,8 @@ Group splitCopy(Handle* h, Group& g, int k0, int kc) {
     const int tc = h->f64 ? 8 : 4;
     for (size_t i = 0; i < h->stages.size(); ++i) {
         ng.cnt[i] = g.cnt[i];
+        ng.statIn = g.statIn;
+        ng.statOut = g.statOut;
         Hist* src[2] = {&g.dev[i].xh, &g.dev[i].uh};
         Hist* dst[2] = {&ng.dev[i].xh, &ng.dev[i].uh};
         for (int k = 0; k < 2; ++k) {
@@ -1095,6 +1114,20 @@ int64_t simulate(Handle* h, Group& g, int64_t n, bool flush, std::vector<int64_t
 }
 
 // Run one group for real: sizes first (so scratch can be sized), then launches.
+// GetStatistics bookkeeping of one successful call (resampler.go:182-322): Process counts its
+// input only when non-empty (the early return of an empty call counts nothing); the cubic
+// engine's Flush returns CubicStage.Flush directly, uncounted (resampler.go:276-279).
+void countStats(const Handle* h, Group& g, int64_t nIn, int64_t nOut, bool flush) {
+    if (!flush) {
+        if (nIn <= 0) return;
+        g.statIn += nIn;
+        g.statOut += nOut;
+        return;
+    }
+    const bool cubicEngine = !h->newPath && h->stages.size() == 1 && h->stages[0]->d.kind == EngineKind::Cubic;
+    if (!cubicEngine) g.statOut += nOut;
+}
+
 int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool flush, hipStream_t s,
                  int64_t cap, gar_status& st) {
     std::vector<int64_t> sizes;
@@ -1106,6 +1139,7 @@ int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool
         std::vector<int64_t> s2;
         OutView o;
         if (flush) chainFlush(x, o, s2); else chainProcess(x, in, o, s2);
+        countStats(h, g, in.n, n, flush);
         return n;
     }
     h->scratchSizes = sizes;
@@ -1113,6 +1147,7 @@ int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool
     std::vector<int64_t> s2;
     const int64_t got = flush ? chainFlush(x, out, s2) : chainProcess(x, in, out, s2);
     if (got != n) { st = GAR_ERR_INTERNAL; g_err = "size mismatch between count and launch"; }
+    else countStats(h, g, in.n, got, flush);
     return got;
 }
 
@@ -1169,7 +1204,10 @@ gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
         }
         return r;
     });
-    if (st == GAR_ERR_DEVICE) h->poisoned = true;
+    if (st == GAR_ERR_DEVICE) {
+        h->poisoned = true;
+        h->failStream = s;
+    }
     return st;
 }
 
@@ -1380,6 +1418,7 @@ gar_status monoCall(Handle* h, int ch, const T* in, int64_t n, T* out, int64_t c
         if (!h->dry) {
             HIPCHK(hipStreamSynchronize(h->stream));
             forSlices(1, got, es + sizeof(T), [&](int, int64_t lo, int64_t hi) { unpackChannel<T>(out, h->f64, ov.p, lo, hi); });
+            trimHost(h);
         }
         if (nOut) *nOut = got;
         return GAR_OK;
@@ -1544,14 +1583,18 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
     return callOn(r, r->stream, [&]() -> gar_status {
         gar_resampler* h = r;
         // exact sizes first: no state changes on BUFFER_TOO_SMALL
+        int64_t need = 0;
         for (auto& g : h->groups) {
             std::vector<int64_t> s;
-            if (simulate(h, g, n, false, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+            const int64_t m = simulate(h, g, n, false, s);
+            if (m > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+            need = std::max(need, m);
         }
         const int C = h->channels;
         const size_t es = h->f64 ? 8 : 4;
-        // planar [channel][frame] in the compute dtype; output rows 16-B aligned (vector stores)
-        const int64_t ocap = (std::max<int64_t>(cap, 1) + 3) / 4 * 4;
+        // planar [channel][frame] in the compute dtype, staged for the exact output length (not the
+        // caller's capacity); output rows 16-B aligned (vector stores)
+        const int64_t ocap = (std::max<int64_t>(need, 1) + 3) / 4 * 4;
         char* hin = nullptr;
         char* hout = nullptr;
         if (!h->dry) {
@@ -1590,6 +1633,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
                 const int64_t m = got[groupOf(h, c) - h->groups.data()];
                 if (lo < m) unpackChannel<double>(out[c], h->f64, hout + static_cast<size_t>(c) * ocap * es, lo, std::min(hi, m));
             });
+            trimHost(h);
         }
         return GAR_OK;
     }, true);
@@ -1600,13 +1644,16 @@ gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch
     if (nch != r->channels) return guard(GAR_ERR_CHANNEL_MISMATCH, "channel count mismatch");
     return callOn(r, r->stream, [&]() -> gar_status {
         gar_resampler* h = r;
+        int64_t need = 0;
         for (auto& g : h->groups) {
             std::vector<int64_t> s;
-            if (simulate(h, g, 0, true, s) > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+            const int64_t m = simulate(h, g, 0, true, s);
+            if (m > cap) return guard(GAR_ERR_BUFFER_TOO_SMALL, "output buffer too small");
+            need = std::max(need, m);
         }
         const int C = h->channels;
         const size_t es = h->f64 ? 8 : 4;
-        const int64_t ocap = (std::max<int64_t>(cap, 1) + 3) / 4 * 4;
+        const int64_t ocap = (std::max<int64_t>(need, 1) + 3) / 4 * 4;
         char* hout = h->dry ? nullptr : static_cast<char*>(h->hostOut.ensure(static_cast<size_t>(ocap) * C * es));
         std::vector<int64_t> got(h->groups.size());
         for (size_t gi = 0; gi < h->groups.size(); ++gi) {
@@ -1629,6 +1676,7 @@ gar_status gar_flush_multi_f64(gar_resampler* r, double* const* out, int32_t nch
                 const int64_t m = got[groupOf(h, c) - h->groups.data()];
                 if (lo < m) unpackChannel<double>(out[c], h->f64, hout + static_cast<size_t>(c) * ocap * es, lo, std::min(hi, m));
             });
+            trimHost(h);
         }
         return GAR_OK;
     }, true);
@@ -1762,15 +1810,17 @@ void gar_reset(gar_resampler* r) {
     DeviceGuard dg(r->dry ? -1 : r->device);
     try {
         if (r->poisoned) {  // recover: drain the handle's streams, fresh state
-            // the failing call recorded no order event, and launches it already queued on a
-            // caller stream may still read the histories and scratch freed below: drain the device
-            (void)hipDeviceSynchronize();
+            // the failing call recorded no order event, and launches it already queued on its
+            // caller stream may still read the histories and scratch freed below: drain that stream
+            // (only the streams this handle enqueued on -- never the whole device)
+            (void)hipStreamSynchronize(r->failStream);
             if (r->stream) (void)hipStreamSynchronize(r->stream);
             if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
             (void)hipGetLastError();
             r->groups.clear();
             r->groups.push_back(freshGroup(r, 0, r->channels));
             r->poisoned = false;
+            r->failStream = nullptr;
             return;
         }
         // one group over every channel: reset in place, keeping its device buffers
@@ -1785,6 +1835,7 @@ void gar_reset(gar_resampler* r) {
                 d.xh.clear();
                 d.uh.clear();
             }
+            g.statIn = g.statOut = 0;
             return;
         }
         if (r->stream) (void)hipStreamSynchronize(r->stream);
@@ -1805,6 +1856,17 @@ int32_t gar_get_latency(const gar_resampler* r) {
 }
 
 int32_t gar_channels(const gar_resampler* r) { return r ? r->channels : 0; }
+
+gar_status gar_get_statistics(const gar_resampler* r, int32_t ch, int64_t* samples_in, int64_t* samples_out) {
+    if (samples_in) *samples_in = 0;
+    if (samples_out) *samples_out = 0;
+    if (!r || ch < 0 || ch >= r->channels) return guard(GAR_ERR_INVALID_ARGUMENT, "channel out of range");
+    const Group* g = groupOf(const_cast<gar_resampler*>(r), ch);
+    if (!g) return guard(GAR_ERR_INTERNAL, "channel without a group");
+    if (samples_in) *samples_in = g->statIn;
+    if (samples_out) *samples_out = g->statOut;
+    return GAR_OK;
+}
 
 gar_status gar_get_info(const gar_resampler* r, gar_info* info) {
     if (!r || !info) return GAR_ERR_INVALID_ARGUMENT;

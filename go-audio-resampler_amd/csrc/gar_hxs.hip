@@ -97,12 +97,17 @@ static void hxsRingFor(const HxDev& p, int G, int& R, int& Rt, int& Wg) {
     R = n * GQ;
     Rt = (R + std::max(0, Wg - GQ) + 15) / 16 * 16;
 }
+// Static LDS of hxs_kernel next to the dynamic ring: the development build's per-wave stamps.
+constexpr size_t kHxsStaticLds = kHxsDev ? sizeof(unsigned long long) * kHxsWaves : 0;
 static bool hxsRingFits(const HxDev& p, int G, int Rt) {
-    return hxsLds(Rt) <= 160 * 1024 && (G * p.Qc + 63) / 64 <= kHxsNP;
+    return hxsLds(Rt) + kHxsStaticLds <= 160 * 1024 && (G * p.Qc + 63) / 64 <= kHxsNP;
 }
 
+// NS values with an instantiated kernel (GAR_HXS_QUICK development builds: only 9 and 10).
+static bool hxsNsBuilt(int ns) { return GAR_HXS_QUICK ? (ns == 9 || ns == 10) : (ns >= 1 && ns <= 10); }
+
 bool hxsPlanFits(const HxDev& p) {
-    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return false;
+    if (!p.rb || p.nw > kHxRbMaxWaves || !hxsNsBuilt(p.NS)) return false;
     int R, Rt, Wg;
     hxsRingFor(p, 1, R, Rt, Wg);
     return hxsRingFits(p, 1, Rt);
@@ -111,7 +116,7 @@ bool hxsPlanFits(const HxDev& p) {
 // hipErrorNotSupported: the plan does not fit this kernel's geometry (the caller uses hx_kernel).
 hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
-    if (!p.rb || p.nw > kHxRbMaxWaves || p.NS < 1 || p.NS > 10) return hipErrorNotSupported;
+    if (!p.rb || p.nw > kHxRbMaxWaves || !hxsNsBuilt(p.NS)) return hipErrorNotSupported;
     static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
     static const int knobWg = std::getenv("GAR_HXS_WGPERCU") ? std::atoi(std::getenv("GAR_HXS_WGPERCU")) : 0;
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;

@@ -89,7 +89,7 @@ EXPORTED = [
     "gar_flush_multi_f64", "gar_process_device", "gar_flush_device", "gar_device_output_size",
     "gar_device_flush_size", "gar_reset", "gar_get_ratio", "gar_get_latency", "gar_get_info", "gar_channels",
     "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite", "gar_profile_enable",
-    "gar_profile_read", "gar_stage_state", "gar_num_stages", "gar_stage_geometry",
+    "gar_profile_read", "gar_stage_state", "gar_num_stages", "gar_stage_geometry", "gar_get_statistics",
 ]
 
 _lib = None
@@ -150,6 +150,7 @@ def lib():
         "gar_stage_state": (i32, [vp, i32, C.POINTER(i32), C.POINTER(i32)]),
         "gar_num_stages": (i32, [vp]),
         "gar_stage_geometry": (i32, [vp, i32, C.POINTER(d), C.POINTER(EngineGeometry)]),
+        "gar_get_statistics": (i32, [vp, i32, C.POINTER(i64), C.POINTER(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -194,11 +195,14 @@ class Resampler:
     def __init__(self, handle, f32_io=False):
         self._h = C.c_void_p(handle)
         self._f32_io = f32_io
+        # bound now: at interpreter exit the module globals (lib) may already be torn down
+        self._free = lib().gar_free
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
-            lib().gar_free(h)
+        free = getattr(self, "_free", None)
+        if h is not None and h.value and free is not None:
+            free(h)
             self._h = None
 
     # -- streaming, channel 0 --
@@ -280,6 +284,12 @@ class Resampler:
 
     def GetLatency(self):
         return lib().gar_get_latency(self._h)
+
+    def GetStatistics(self, channel=0):
+        """engine.Resampler.GetStatistics (internal/engine/resampler.go:348-353)."""
+        a, b = C.c_int64(0), C.c_int64(0)
+        _check(lib().gar_get_statistics(self._h, channel, C.byref(a), C.byref(b)))
+        return {"samplesIn": a.value, "samplesOut": b.value}
 
     def GetInfo(self):
         info = Info()

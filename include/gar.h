@@ -190,6 +190,11 @@ double gar_get_ratio(const gar_resampler *r);           /* GetRatio (constant.go
 int32_t gar_get_latency(const gar_resampler *r);        /* GetLatency (constant.go:407-426) */
 gar_status gar_get_info(const gar_resampler *r, gar_info *info); /* GetInfo (constant.go:452-485) */
 int32_t gar_channels(const gar_resampler *r);
+/* GetStatistics (internal/engine/resampler.go:348-353; SimpleResampler{,Float32}.GetStatistics
+ * convenience.go:184-187,393-396): samplesIn / samplesOut of channel `ch`'s engine -- input frames of
+ * every non-empty Process, output frames of every Process and Flush (the QualityQuick engine's Flush
+ * is uncounted, resampler.go:276-279), both zeroed by Reset.  GAR_ERR_INVALID_ARGUMENT for a bad ch. */
+gar_status gar_get_statistics(const gar_resampler *r, int32_t ch, int64_t *samples_in, int64_t *samples_out);
 const char *gar_status_string(gar_status s);
 const char *gar_last_error(void);                       /* thread-local detail for the last failure */
 /* HIP-event timing of every MFMA FIR launch (bracketed on its own stream). */

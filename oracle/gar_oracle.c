@@ -383,6 +383,12 @@ API void o_engine_reset(o_engine *e) {
     if (e->is_f32) resampler_reset_f((resampler_f *)e->r); else resampler_reset_d((resampler_d *)e->r);
 }
 
+/* GetStatistics (resampler.go:348-353): out[0] = samplesIn, out[1] = samplesOut */
+API void o_engine_stats(o_engine *e, int64_t *out) {
+    if (e->is_f32) { out[0] = ((resampler_f *)e->r)->samples_in; out[1] = ((resampler_f *)e->r)->samples_out; }
+    else { out[0] = ((resampler_d *)e->r)->samples_in; out[1] = ((resampler_d *)e->r)->samples_out; }
+}
+
 API double o_engine_ratio(o_engine *e) {
     return e->is_f32 ? ((resampler_f *)e->r)->ratio : ((resampler_d *)e->r)->ratio;
 }

@@ -59,7 +59,7 @@ def lib():
             "o_design_polyphase_filter": (i, [i, d, d, i, i, vp]), "o_is_integer_ratio": (i, [d]),
             "o_engine_new": (vp, [d, d, i, i]), "o_engine_free": (None, [vp]),
             "o_engine_process": (i64, [vp, vp, i64, vp, i64]), "o_engine_flush": (i64, [vp, vp, i64]),
-            "o_engine_reset": (None, [vp]), "o_engine_ratio": (d, [vp]),
+            "o_engine_reset": (None, [vp]), "o_engine_ratio": (d, [vp]), "o_engine_stats": (None, [vp, vp]),
             "o_engine_get_info": (None, [vp, C.POINTER(EngineInfo)]),
             "o_engine_get_coeffs": (i64, [vp, i, i, vp]),
             "o_precision_to_engine_quality": (i, [i]), "o_preset_to_engine_quality": (i, [i]),
@@ -186,6 +186,12 @@ class Engine:
 
     def reset(self):
         lib().o_engine_reset(self.h)
+
+    def statistics(self):
+        """GetStatistics (resampler.go:348-353)."""
+        v = np.zeros(2, dtype=np.int64)
+        lib().o_engine_stats(self.h, _ptr(v))
+        return {"samplesIn": int(v[0]), "samplesOut": int(v[1])}
 
     @property
     def ratio(self):

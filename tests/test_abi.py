@@ -109,6 +109,41 @@ def test_engine_stream_lengths(gar, O, i, o, preset):
             assert a == b, (n, a, b)
 
 
+@pytest.mark.parametrize("i,o", [(44100, 48000), (48000, 44100), (96000, 48000), (48000, 96000), (16000, 44100)])
+@pytest.mark.parametrize("preset", [0, 3])
+def test_engine_statistics(gar, O, i, o, preset):
+    """GetStatistics (resampler.go:348-353) after every call of a chunked stream with flushes,
+    an empty Process and a Reset equals the reference engine's samplesIn / samplesOut."""
+    rng = np.random.default_rng(3)
+    e = O.Engine(i, o, O.lib().o_preset_to_engine_quality(preset))
+    r = gar.NewEngineDry(i, o, preset)
+    assert r.GetStatistics() == {"samplesIn": 0, "samplesOut": 0}
+    for n in [4096, 1, 0, 777, "f", 4800, "f", "reset", 333, 20000, "f"]:
+        if n == "f":
+            e.flush(), r.Flush()
+        elif n == "reset":
+            e.reset(), r.Reset()
+        else:
+            x = rng.standard_normal(n)
+            e.process(x), r.Process(x)
+        assert r.GetStatistics() == e.statistics(), n
+    with pytest.raises(gar.ResamplerError):
+        r.GetStatistics(channel=1)
+
+
+def test_statistics_per_channel_group(gar):
+    """A mono Process on a multi-channel handle advances channel 0 alone (constant.go:88-95):
+    its counters move, the other channels' do not."""
+    g = gar.New(gar.Config(44100, 48000, 2, gar.QualityHigh, DryRun=True))
+    g.ProcessMulti([np.zeros(1000), np.zeros(1000)])
+    both = g.GetStatistics(0)
+    assert both == g.GetStatistics(1) and both["samplesIn"] == 1000
+    g.Process(np.zeros(500))
+    assert g.GetStatistics(0)["samplesIn"] == 1500 and g.GetStatistics(1)["samplesIn"] == 1000
+    g.Reset()
+    assert g.GetStatistics(0) == {"samplesIn": 0, "samplesOut": 0} == g.GetStatistics(1)
+
+
 NEW_PAIRS = [(44100, 48000), (48000, 44100), (96000, 44100), (96000, 16000), (192000, 48000), (48000, 8000),
              (88200, 16000), (44100, 44200), (16000, 48000), (8000, 96000)]
 

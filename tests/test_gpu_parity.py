@@ -229,6 +229,35 @@ def test_process_multi_and_flush_multi(gar, O, cuda):  # parallel_test.go:12-89,
         check(np.concatenate([outs[c], tails[c]]), want[c], F64_RMS_TOL)
 
 
+def test_concurrent_handles_large_host_calls(gar, cuda):
+    """Two threads drive two independent handles with host ProcessMulti calls large enough
+    (> 1 MiB) to use the shared packing pool (ctypes releases the GIL): each thread's outputs
+    equal the same calls made alone, bit for bit (Go resampler instances are independent)."""
+    import threading
+    xs = [signal(96000, 4, 48000, seed=s) for s in (11, 12)]
+
+    def run(x, out, reps=4):
+        r = gar.New(gar.Config(48000, 44100, 4, gar.QualityHigh, ComputeDtype=gar.F32))
+        for _ in range(reps):
+            r.Reset()
+            res = r.ProcessMulti([x[:, c] for c in range(4)])
+            out.append(np.concatenate(res + r.FlushMulti()))
+
+    alone = [[], []]
+    for k in range(2):
+        run(xs[k], alone[k], reps=1)
+    both = [[], []]
+    th = [threading.Thread(target=run, args=(xs[k], both[k])) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for k in range(2):
+        assert len(both[k]) == 4
+        for got in both[k]:
+            np.testing.assert_array_equal(got, alone[k][0])
+
+
 def test_mono_call_on_multichannel_handle(gar, O, cuda):
     """Process advances channel 0 only (constant.go:88-95); ProcessMulti after it."""
     x = signal(9000, 2, 48000, seed=4)

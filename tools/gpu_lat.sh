@@ -2,7 +2,7 @@
 # Small-launch latency probes: streaming calls and cfg5 chunks, kernarg placement, dev phase stamps.
 O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O; L=$O/lat.log; : > $L
 D=$GRAFT_REPO_ROOT/go-audio-resampler_amd/libgar_dev.so
-run() { echo "== $*" >> $L; env "$@" 2>&1 | grep -v "amdgpu.ids\|^bg:\|Exception ignored\|Traceback\|File \"\|TypeError" >> $L; }
+run() { echo "== $*" >> $L; env "$@" >> $L 2>&1; }
 run P_N=600 timeout -k 10 60 python tools/stream_probe.py || exit 1
 run HIP_FORCE_DEV_KERNARG=1 P_N=600 timeout -k 10 60 python tools/stream_probe.py || exit 1
 run HIP_FORCE_DEV_KERNARG=0 P_N=600 timeout -k 10 60 python tools/stream_probe.py || exit 1
