@@ -146,7 +146,7 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // Sets a kernel's 160 KiB dynamic-LDS attribute once per (device, kernel):
 // the attribute is per device, and handles on several devices may launch
 // from several host threads (gar_kernels.hip).
-void setMaxLdsOnce(const void* fn);
+size_t setMaxLdsOnce(const void* fn);  // raises the kernel's dynamic-LDS limit; returns the limit in force
 
 // Input element kk of column `col`'s window (column = channel c, chunk of G
 // macro periods).  Fast path when the whole window lies in one buffer.
@@ -585,6 +585,106 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcD
     if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
 }
 
+// Small launches of row-block-aligned plans, time-major (default; bg_rb_kernel is the GAR_BG_RT=0
+// fallback): workgroup v = (row block rb, channel c, chunk block kb) -- the 16 columns are 16
+// consecutive macro periods of ONE channel, so their windows overlap: the union window (15*Qc +
+// Kread rows of channel c) is staged once in LDS by all waves (one memory round trip of ~4 loads
+// per thread instead of every wave gathering NS rows of 16 columns), then wave w runs program
+// rbStart[rb] + w with B read from LDS.  LDS rows are padded by kRtPad(Qc) every Qc rows so the 16
+// columns of a B read (Qc rows apart) fall on distinct bank pairs.  Same A, same B values, same
+// MFMA order and program-order reduction as bg_kernel / bg_rb_kernel: the same bits.
+__host__ __device__ constexpr int kRtPad(int Qc) { return ((2 - Qc) % 32 + 32) % 32; }  // (Qc + pad) % 32 == 2
+inline size_t bgRtLds(int Qc, int Kread, int nprog, size_t esz) {
+    const int nrow = 15 * Qc + Kread;
+    const size_t win = (static_cast<size_t>(nrow) + static_cast<size_t>(kRtPad(Qc)) * (nrow / Qc + 1)) * esz;
+    return (win + 15) / 16 * 16 + static_cast<size_t>(nprog) * 64 * 4 * esz;
+}
+
+template <class TC, int NS>
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+    typedef typename Acc<TC>::V V;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wt = threadIdx.x >> 6;
+    const TC* Aimg = static_cast<const TC*>(p.A);
+    const int Qc = g.Qc, pad = kRtPad(Qc);
+    const int nrow = 15 * Qc + g.Wl;  // union window of 16 macro periods (Wl = Kread)
+    const int nphys = nrow + pad * (nrow / Qc + 1);
+    TC* win = reinterpret_cast<TC*>(smem);
+    V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(nphys) * sizeof(TC) + 15) / 16 * 16);
+    const int nkb = (g.nchunk + 15) / 16;
+    const int nv = p.nrb * g.C * nkb;
+    const bool same = srcSameType<TC>(src);
+    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
+        const int rb = v % p.nrb, cb = v / p.nrb;
+        const int c = cb / nkb, kb = cb - c * nkb;
+        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
+        TC A[NS];
+        int k0 = 0;
+        if (wt < np) {  // A lands while the window is staged
+            const int pr = ps + wt;
+            k0 = g.rbK0[pr];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+        }
+        // stage rows [0, nrow) of channel c from T: batches of 4 loads per thread in flight
+        const int64_t T = (g.a_lo + 16 * static_cast<int64_t>(kb)) * Qc;
+        for (int r0 = threadIdx.x; r0 < nrow; r0 += 4 * blockDim.x) {
+            TC vv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = r0 + u * blockDim.x;
+                vv[u] = same ? srcReadBF<TC>(src, T + r, c, r < nrow, Aimg) : (r < nrow ? srcRead<TC>(src, T + r, c) : TC(0));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = r0 + u * blockDim.x;
+                if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
+            }
+        }
+        if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside the staging
+        __syncthreads();  // window staged
+        const int n = lane & 15, kq = lane >> 4;
+        const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
+        const bool colOk = 16 * kb + n < g.nchunk;
+        V r = {0, 0, 0, 0};
+        if (wt < np) {
+            // row n*Qc + k0 + 4s + kq -> LDS index n*(Qc+pad) + x + pad*(x / Qc), x = k0 + 4s + kq
+            const int x0 = k0 + kq;
+            int q = x0 / Qc, rem = x0 - q * Qc;
+            const int nb = n * (Qc + pad);
+            TC B[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                B[s] = win[nb + q * (Qc + pad) + rem];
+                rem += 4;
+                if (rem >= Qc) { rem -= Qc; ++q; }
+            }
+            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+            }
+            r = acc0 + acc1;
+            if (np > 1) slots[wt * 64 + lane] = r;
+        }
+        if (np > 1) {
+            __syncthreads();
+            if (wt == 0) {
+                V sum = slots[lane];
+                for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
+                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            }
+        } else if (wt == 0 && !(g.dbg & 2)) {
+            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        }
+        __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
+    }
+    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;  // the first row block of this workgroup
+    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
+}
+
 template <class TC, int NS>
 static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                              size_t lds, int64_t blocks, hipStream_t st, bool globalB) {
@@ -596,7 +696,12 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
     if (g.rbMode) {
         if constexpr (sizeof(TC) == 8 && NS <= kBgRbMaxSteps) {
             if (threads > 64 * kBgRbMaxWaves) return hipErrorInvalidConfiguration;
-            hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
+            if (g.rbMode == 2) {  // time-major, LDS-staged windows
+                if (setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)) < lds) return hipErrorOutOfMemory;
+                hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
+            } else {
+                hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
+            }
             return hipGetLastError();
         }
         return hipErrorNotSupported;

@@ -8,7 +8,7 @@
 #include <utility>
 #include <vector>
 
-#include "gar_hxs.hpp"
+#include "gar_hxt.hpp"
 
 namespace gar {
 
@@ -16,6 +16,11 @@ namespace gar {
 #define GAR_HXS_EXT(NS, V) extern template hipError_t hxsLaunch<NS, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
 GAR_HXS_FOR_ALL(GAR_HXS_EXT)
 #undef GAR_HXS_EXT
+// hxt_kernel instantiations: gar_hxt_i1.hip / gar_hxt_i2.hip
+#define GAR_HXT_EXT(NS, F, V) extern template hipError_t hxtLaunch<NS, F, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+GAR_HXT_FOR_A(GAR_HXT_EXT)
+GAR_HXT_FOR_B(GAR_HXT_EXT)
+#undef GAR_HXT_EXT
 
 namespace {
 constexpr int kProfWords = 64 + 2 * 4096;
@@ -71,6 +76,35 @@ unsigned long long* profBuf() {
 
 int64_t fdiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
+
+template <int NS>
+hipError_t hxtFmt(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    if (x.fmt == 1 && x.vst == 2) return hxtLaunch<NS, 1, 2>(x, lds, blocks, st);
+    if (x.fmt == 2 && x.vst == 0) return hxtLaunch<NS, 2, 0>(x, lds, blocks, st);
+    if (x.fmt == 2 && x.vst == 1) return hxtLaunch<NS, 2, 1>(x, lds, blocks, st);
+    return hipErrorNotSupported;
+}
+
+// Compute-wave roles of hxt_kernel for nprog row blocks (HxsArgs::role): the first 4*floor(nprog/4)
+// row blocks one wave each; one remaining row block shared by 4 waves (every 4th period), two by
+// 2 waves each (every 2nd period), so waves w, w+4, w+8 -- one SIMD -- carry equal MFMA work.
+// Returns the compute wave count; *maxStride the largest period stride.
+static int hxtRoles(int nprog, int* role, int* maxStride) {
+    const int q = nprog / 4 * 4, r = nprog - q;
+    int w = 0;
+    *maxStride = 1;
+    for (int i = 0; i < q; ++i) role[w++] = i | (1 << 16);
+    if (r == 2 && q + 4 <= kHxtMaxComp) {
+        for (int i = 0; i < 4; ++i) role[w++] = (q + (i & 1)) | ((i >> 1) << 8) | (2 << 16);
+        *maxStride = 2;
+    } else if (r == 1 && q + 4 <= kHxtMaxComp) {
+        for (int i = 0; i < 4; ++i) role[w++] = q | (i << 8) | (4 << 16);
+        *maxStride = 4;
+    } else {
+        for (int i = q; i < nprog; ++i) role[w++] = i | (1 << 16);
+    }
+    return w;
+}
 
 template <int NS>
 hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
@@ -167,15 +201,38 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     } else if ((inA & 15) == 0 && C % 16 == 0 && src.in_cs == 1 && src.in_fs % 4 == 0) {
         fmt = 2;
     }
+    // output layout of the epilogue (hxsStoreFast VST), see below
+    const int esz = od.pcm ? pcmBytes(od.pcm) : (od.f64 ? 8 : 4);
+    char* const outBase = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(od.out) - static_cast<uintptr_t>(od.o0 * od.fs * esz));
+    const bool al = (reinterpret_cast<uintptr_t>(outBase) & 15) == 0;
+    int vst;
+    if (od.pcm == 16 && al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) vst = 4;  // int16 stereo frame pairs
+    else if (od.pcm) vst = 0;  // other PCM stores: the epilogue's checked per-element path
+    else if (od.f64) vst = 3;
+    else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) vst = 2;
+    else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) vst = 1;
+    else vst = 0;
+
+    // balanced kernel (hxt_kernel): f32 stereo frames or 16-channel rows in, f32 out (knob GAR_HXT=0: hxs_kernel)
+    static const int knobHxt = std::getenv("GAR_HXT") ? std::atoi(std::getenv("GAR_HXT")) : 0;
+    int role[kHxtMaxComp] = {}, maxStride = 1, ncomp = 0;
+    const bool hxt = knobHxt && !small && !od.pcm && !od.f64 && !src.in_pcm &&
+                     ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
+    if (hxt) ncomp = hxtRoles(p.nw, role, &maxStride);
+
     int G = 0, R = 0, Rt = 0, Wg = 0;
-    for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
-        int r, rt, wg;
-        hxsRingFor(p, cand, r, rt, wg);
-        if (cand > 1 && cand > Np) continue;
-        if (knobG > 0 && cand > knobG && cand > 1) continue;
-        if (!hxsRingFits(p, cand, rt)) continue;
-        G = cand; R = r; Rt = rt; Wg = wg;
-        break;
+    for (int pass = hxt && maxStride > 1 ? 0 : 1; pass < 2 && G == 0; ++pass) {  // hxt: G a multiple of the stride first
+        for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
+            int r, rt, wg;
+            hxsRingFor(p, cand, r, rt, wg);
+            if (cand > 1 && cand > Np) continue;
+            if (knobG > 0 && cand > knobG && cand > 1) continue;
+            if (!hxsRingFits(p, cand, rt)) continue;
+            if (hxt && cand * Qc > kHxtMaxRows) continue;
+            if (pass == 0 && cand % maxStride != 0) continue;
+            G = cand; R = r; Rt = rt; Wg = wg;
+            break;
+        }
     }
     if (G == 0) return hipErrorNotSupported;
 
@@ -214,19 +271,14 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.nt = knobNt;
     x.xcdPair = knobPair && fmt == 2 && (C / 16) % 2 == 0 && x.nblocks % 16 == 0 ? 1 : 0;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
-    const int esz = od.pcm ? pcmBytes(od.pcm) : (od.f64 ? 8 : 4);
     x.out_pcm = od.pcm;
     x.out_f64 = od.f64;
-    x.out = reinterpret_cast<char*>(reinterpret_cast<uintptr_t>(od.out) - static_cast<uintptr_t>(od.o0 * od.fs * esz));
+    x.out = outBase;
     x.out_fs = od.fs * esz;
     x.out_cs = od.cs * esz;
-    const bool al = (reinterpret_cast<uintptr_t>(x.out) & 15) == 0;
-    if (od.pcm == 16 && al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 4;  // int16 stereo frame pairs
-    else if (od.pcm) x.vst = 0;  // other PCM stores: the epilogue's checked per-element path
-    else if (od.f64) x.vst = 3;
-    else if (al && C == 2 && od.fs == 2 && od.cs == 1 && Pc % 4 == 0) x.vst = 2;
-    else if (al && od.fs == 1 && (od.cs * 4) % 16 == 0 && Pc % 4 == 0) x.vst = 1;
-    else x.vst = 0;
+    x.vst = vst;
+    x.ncomp = ncomp;
+    for (int w = 0; w < kHxtMaxComp; ++w) x.role[w] = role[w];
     x.src = src;
     x.od = od;
     x.rows = p.rows;
@@ -241,8 +293,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.T1 = p.T1;
     x.T2 = p.T2;
     if (trace)
-        fprintf(stderr, "hxs: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
-                x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
+        fprintf(stderr, "%s: small=%d o[%lld,%lld) C=%d G=%d Np=%lld ngroups=%d nblocks=%d R=%d Rt=%d Wg=%d fmt=%d vst=%d fast[%lld,%lld)\n",
+                hxt ? "hxt" : "hxs", x.small, (long long)od.o_lo, (long long)od.o_hi, C, G, (long long)Np, x.ngroups, x.nblocks, R, Rt, Wg, x.fmt, x.vst,
                 (long long)x.fastLo, (long long)x.fastHi);
     if (hc && hc->n > 0 && hc->dst) {  // history keep folded into this launch (no gather_kernel after it)
         x.hdst = static_cast<float*>(hc->dst);
@@ -252,6 +304,19 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     }
     const size_t lds = hxsLds(Rt);
     const int64_t blocks = x.nblocks;
+    if (hxt) {
+        const int64_t hblocks = blocks;
+        switch (p.NS) {
+#define GAR_HXT_NS(n) case n: return hxtFmt<n>(x, lds, hblocks, stream);
+#if !GAR_HXS_QUICK
+            GAR_HXT_NS(1) GAR_HXT_NS(2) GAR_HXT_NS(3) GAR_HXT_NS(4) GAR_HXT_NS(5) GAR_HXT_NS(6) GAR_HXT_NS(7)
+            GAR_HXT_NS(8)
+#endif
+            GAR_HXT_NS(9) GAR_HXT_NS(10)
+#undef GAR_HXT_NS
+            default: return hipErrorNotSupported;
+        }
+    }
     switch (p.NS) {
 #define GAR_HXS_NS(n) case n: return hxsVst<n>(x, lds, blocks, stream);
 #if !GAR_HXS_QUICK

@@ -101,6 +101,10 @@ struct HxsArgs {
     const double* polyA;
     const double* dftC;
     int T1, T2;
+    // hxt_kernel (gar_hxt.hpp): compute wave w runs row block role[w] & 0xff on the periods p with
+    // p % stride == phase (phase = (role[w] >> 8) & 0xff, stride = role[w] >> 16)
+    int ncomp;
+    int role[12];
 };
 typedef const __attribute__((address_space(4))) HxsArgs* HxsArgsP;
 
@@ -937,11 +941,11 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
 template <int NS, int VST>
 hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
     if (x.small && !x.bigSmall) {
-        setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>));
+        if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
         hipLaunchKernelGGL((hxs_small_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * x.nprog), lds, st, x);
         return hipGetLastError();
     }
-    setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>));
+    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
     hipLaunchKernelGGL((hxs_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.nprog + kHxsLoaders)), lds, st, x);
     return hipGetLastError();
 }

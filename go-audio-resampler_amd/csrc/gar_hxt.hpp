@@ -1,0 +1,469 @@
+// gar_hxt.hpp -- balanced streaming split-f16 FIR kernel (row-block plans, gfx950).
+//
+// Same arithmetic, ring image and per-output MFMA order as hxs_kernel (gar_hxs.hpp), so the two
+// kernels (and hxs_small_kernel / hx_kernel) produce identical bits; what changes is how the work
+// of a workgroup maps onto the CU's four SIMDs:
+//
+//  * Balanced compute waves.  hxs_kernel runs one compute wave per row block, so a 10-row-block
+//    plan puts 3/3/2/2 MFMA streams on the four SIMDs and the busiest SIMD sets the pace (+20 %).
+//    Here the host hands every compute wave a role (row block, period phase, period stride): the
+//    first 4*floor(nprog/4) row blocks get one wave each (stride 1), and the remaining one or two
+//    row blocks are each shared by 4 / 2 waves that take every 4th / 2nd macro period.  Waves w,
+//    w+4, w+8 share a SIMD (a workgroup's waves are dealt round-robin over the SIMDs), so every
+//    SIMD carries the same number of MFMA steps per period: 10 row blocks -> 12 compute waves,
+//    9 + 9 + 4.5 steps per SIMD.  Each output is still computed by exactly one wave with the same
+//    A fragments and MFMA chain, so the bits do not change.
+//  * One loader wave per SIMD (4), each specialised at compile time for the launch's input layout
+//    (FMT 1 stereo f32 frames, FMT 2 rows of 16 f32 channels): a fixed buffer-load pattern issued
+//    kHxtD groups ahead into registers, then a straight-line f16 hi/lo split into the ring with the
+//    loud-element test folded into one running integer max per lane (the exact per-element path
+//    runs only when that max says a loud element is present).  Edge loads (history seam, stream
+//    start, partial blocks) go through an out-of-line gather, so their code does not weigh on the
+//    registers of the streaming loop.
+//  * Groups never run past the chunk (the last group of a chunk has Np - g*G periods).
+#pragma once
+#include "gar_hxs.hpp"
+
+namespace gar {
+
+constexpr int kHxtLoaders = 4;                          // one loader wave per SIMD
+constexpr int kHxtMaxComp = 12;                         // compute waves (3 per SIMD)
+constexpr int kHxtWaves = kHxtMaxComp + kHxtLoaders;    // __launch_bounds__: 16 waves, 128 VGPRs
+constexpr int kHxtD = 2;                                // loads in flight per loader (register staging)
+constexpr int kHxtItems = 10;                           // items per loader per load
+constexpr int kHxtMaxRows = 64 * kHxtItems;             // rows of one load (G*Qc): FMT 1 quad l = loader l,
+                                                        // 64-row pieces; FMT 2 16-row pieces l, l+4, ...
+constexpr uint32_t kHxtLoudBits = 0x41800000u;          // bits(16.0f): |x| >= 16, Inf, NaN <=> (bits & 0x7fffffff) >= it
+
+struct HxtRole {
+    int rb, ph, st;
+};
+__device__ __forceinline__ HxtRole hxtRole(const HxsArgs& x, int w) {
+    const int r = uni(x.role[w]);
+    return HxtRole{r & 0xff, (r >> 8) & 0xff, r >> 16};
+}
+
+// ---- loaders ------------------------------------------------------------------------
+template <int FMT>
+struct HxtBuf;
+template <>
+struct HxtBuf<1> {  // stereo f32 frames: two chunks (both channels each) per item
+    f2v a[kHxtItems], b[kHxtItems];
+};
+template <>
+struct HxtBuf<2> {  // 16-channel f32 rows: four channels of one row per lane
+    f32x4 v[kHxtItems];
+};
+
+// Issue load `st` (a real load when live and fast; otherwise every item's offset lies past the
+// records, which returns zeros without a memory access -- the same instruction pattern on every
+// path, so the compiler's vmcnt tracking waits for exactly the oldest load).
+template <int FMT>
+__device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxtBuf<FMT>& r) {
+    const bool fast = live && st.fast;
+    const int nrow = fast ? st.nrow : 0;
+    const int base = st.T0 * rs.rowB + rs.lane0;
+#pragma unroll
+    for (int k = 0; k < kHxtItems; ++k) {
+        if constexpr (FMT == 1) {  // quad l = chunks 2l, 2l+1; piece k = rows 64k ..
+            const bool on = 64 * k < nrow;
+            const int o = on ? base + 64 * k * rs.rowB + 2 * l * rs.chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + rs.chunkB : o;
+            r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
+            r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
+        } else {  // 16-row piece l + 4k, lane = 16 quad + row
+            const int it = l + kHxtLoaders * k;
+            const bool on = 16 * it < nrow;
+            const int o = on ? base + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
+            r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
+        }
+    }
+    return fast;
+}
+
+// One ring row (quad q, ring row p) <- hi/lo split of e; the mirror copy when p < mirror.
+__device__ __forceinline__ void hxtPut(char* qb, uint32_t dL, int p, int R, int mirror, f32x4 e) {
+    uint2 hv, lv;
+    hxSplit2(e[0], e[1], hv.x, lv.x);
+    hxSplit2(e[2], e[3], hv.y, lv.y);
+    *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
+    *reinterpret_cast<uint2*>(qb + dL + 8 * p) = lv;
+    if (p < mirror) {
+        *reinterpret_cast<uint2*>(qb + 8 * (p + R)) = hv;
+        *reinterpret_cast<uint2*>(qb + dL + 8 * (p + R)) = lv;
+    }
+}
+
+__device__ __forceinline__ uint32_t hxtMag(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+
+template <int FMT>
+__device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT>& r, int k) {
+    if constexpr (FMT == 1) return f32x4{r.a[k].x, r.a[k].y, r.b[k].x, r.b[k].y};
+    else return r.v[k];
+}
+
+// Exact per-element path of a load that holds a loud element (rare, out of line): loader l's items
+// of the load again, re-read from memory through the SrcDesc with the fast path's item mapping and
+// staged through hxsPutItem (loud elements as zero, their column rows recorded).
+template <int FMT>
+__device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
+    const SrcDesc src = kload(&xp->src);
+    const int p0 = uni(st.T0 % xp->R);
+    for (int k = 0; k < kHxtItems; ++k) {
+        int row, q;
+        if constexpr (FMT == 1) {
+            if (64 * k >= st.nrow) break;
+            row = 64 * k + lane;
+            q = l;
+        } else {
+            const int it = l + kHxtLoaders * k;
+            if (16 * it >= st.nrow) break;
+            row = 16 * it + (lane & 15);
+            q = lane >> 4;
+        }
+        if (row >= st.nrow) continue;
+        f32x4 e;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int col = b * 16 + 4 * q + n;
+            const int kk = col / xp->C, c = col - kk * xp->C;
+            e[n] = hxsGather(src, hxsChunkRow(xp, kk, st.T0 + row), c, xp->A);
+        }
+        hxsPutItem(xp, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+    }
+}
+
+// Edge load (rows before the raw input, partial blocks, any other layout): every element gathered
+// through the SrcDesc (history | input | zeros); out of line.  Loader l takes items l, l+4, ...
+// of the 4 quads x ceil(nrow/64) pieces.
+__device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
+    const SrcDesc src = kload(&xp->src);
+    const int p0 = uni(st.T0 % xp->R);
+    const int nit = 4 * ((st.nrow + 63) >> 6);
+    for (int it = l; it < nit; it += kHxtLoaders) {
+        const int q = it & 3, row = 64 * (it >> 2) + lane;
+        if (row >= st.nrow) continue;
+        f32x4 e;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            const int col = b * 16 + 4 * q + n;
+            const int kk = col / xp->C, c = col - kk * xp->C;
+            e[n] = col < xp->ncols ? hxsGather(src, hxsChunkRow(xp, kk, st.T0 + row), c, xp->A) : 0.f;
+        }
+        hxsPutItem(xp, st, p0, q, row, e, sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+    }
+}
+
+// Fast load `st` -> ring (registers of its issue): split, write, one running max for the loud test.
+template <int FMT>
+__device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, const HxtBuf<FMT>& r, int b, int l,
+                                           int lane, const HxsShared& sh) {
+    const int R = x.R, mirror = x.mirror;
+    const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
+    const int p0 = uni(st.T0 % R);
+    const int nrow = st.nrow;
+    // opaque per call: the compiler must not hoist the items' row numbers out of the step loop
+    // (ten live row registers spill, and every reload's vmcnt(0) waits for the loads in flight)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kHxtItems; ++k) {
+        int row, q;
+        bool on;
+        if constexpr (FMT == 1) {
+            on = 64 * k < nrow;
+            row = 64 * k + ln;
+            q = l;
+        } else {
+            const int it = l + kHxtLoaders * k;
+            on = 16 * it < nrow;
+            row = 16 * it + (ln & 15);
+            q = ln >> 4;
+        }
+        if (on) {  // uniform
+            const f32x4 e = hxtItem<FMT>(r, k);
+            m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
+            int p = p0 + row;
+            p = p >= R ? p - R : p;
+            if (row < nrow) hxtPut(sh.ring + q * sh.QS, dL, p, R, mirror, e);
+        }
+    }
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
+        hxtLoudLoad<FMT>(hxsCold(), st, b, l, lane, sh);
+}
+
+// ---- progress counters (LDS) -------------------------------------------------------------
+// Inside a block no workgroup barrier is taken: loader l publishes ld[l] = loads converted, compute
+// wave w publishes cp[w] = groups finished.  Group g may run once every loader has converted loads
+// 0 .. P+g-1 (its window); load j may overwrite ring rows once every compute wave has finished the
+// last group whose window held them.  A wave publishes after s_waitcnt lgkmcnt(0) (its ring writes
+// / reads done), and LDS executes one wave's operations in order, so a reader that sees the count
+// and then reads the ring sees the data.  Waits are bounded (a wrong count ends the wait after
+// ~2^24 polls with wrong output instead of a hung GPU).
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) int lds_i32;
+typedef __attribute__((address_space(3))) i32x4v lds_i32x4;
+// Explicit LDS pointers: a generic pointer makes the polls flat loads, and a flat load's
+// s_waitcnt vmcnt(0) waits for every store the wave has in flight.
+struct HxtSync {
+    lds_i32* ld;  // [kHxtLoaders]
+    lds_i32* cp;  // [kHxtMaxComp]
+};
+
+__device__ __forceinline__ void hxtPublish(lds_i32* slot, int v, int lane) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring writes / reads done
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) *reinterpret_cast<volatile lds_i32*>(slot) = v;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// min(cnt[0 .. n)) >= need, n <= 12 (16-B aligned counters, read as int4).
+__device__ __forceinline__ void hxtWait(const lds_i32* cnt, int n, int need) {
+    for (int it = 0; it < (1 << 24); ++it) {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        const i32x4v a = *reinterpret_cast<const volatile lds_i32x4*>(cnt);
+        int m = min(min(a.x, a.y), min(a.z, a.w));
+        if (n > 4) {
+            const i32x4v b = *reinterpret_cast<const volatile lds_i32x4*>(cnt + 4);
+            m = min(m, min(min(b.x, b.y), min(b.z, b.w)));
+        }
+        if (n > 8) {
+            const i32x4v c = *reinterpret_cast<const volatile lds_i32x4*>(cnt + 8);
+            m = min(m, min(min(c.x, c.y), min(c.z, c.w)));
+        }
+        if (m >= need) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Groups of a block whose windows a load must not overwrite: load j >= P writes column rows
+// [Wg + (j-P)*GQ, + GQ), whose previous occupants (rows - R) belong to groups <= the returned index.
+__device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
+    const int GQ = x.G * x.Qc;
+    const int last = x.Wg + (j - P + 1) * GQ - 1 - x.R;  // highest overwritten row, previous lap
+    return last < 0 ? 0 : last / GQ + 1;                 // groups 0 .. last/GQ must be finished
+}
+
+// Loader wave l: in step j it waits for the ring rows of load j to be free, converts load j
+// (issued kHxtD steps earlier) into the ring, publishes it and issues load j + kHxtD into the
+// registers just freed.
+template <int FMT>
+__device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
+                                           int lane) {
+    const HxsArgsP xp = hxsCold();
+    const int GQ = x.G * x.Qc;
+    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
+    const int nstepsPad = hxsStepsPad(x);
+    const int dbg = kHxsDev ? x.dbg : 0;
+    HxtBuf<FMT> buf[kHxtD];
+    bool fastL[kHxtD];
+    const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
+#pragma unroll
+    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT>(hxsLoad(xp, b, d, P), d < nL, rs, l, buf[d]);
+    for (int j0 = 0; j0 < nstepsPad; j0 += kHxtD) {
+#pragma unroll
+        for (int d = 0; d < kHxtD; ++d) {
+            const int j = j0 + d;
+            if (j < nL) {
+                if (j >= P) hxtWait(sy.cp, x.ncomp, hxtFreeNeed(x, j, P));
+                if (!((dbg & 16) && j >= P)) {
+                    const HxsStage st = hxsLoad(xp, b, j, P);
+                    if (fastL[d]) hxtConvert<FMT>(x, st, buf[d], b, l, lane, sh);
+                    else hxtGatherLoad(xp, st, b, l, lane, sh);
+                }
+                hxtPublish(sy.ld + l, j + 1, lane);
+            }
+            fastL[d] = hxtIssue<FMT>(hxsLoad(xp, b, j + kHxtD, P), j + kHxtD < nL && !((dbg & 1) && j >= P), rs, l,
+                                     buf[d]);
+        }
+    }
+}
+
+// ---- compute waves ----------------------------------------------------------------------
+// Group g: wait for its window, run this wave's periods p = first, first + st, ... < end
+// (chunk-relative), publish.  One accumulator pair per period: with three compute waves per SIMD
+// the other waves cover a period's MFMA drain before its epilogue.
+template <int NS, int VST, bool FAST>
+__device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int wt, int lane,
+                                          const h8v (&Ah)[NS], const h8v (&Al)[NS], uint32_t laneOff, int u0, int P,
+                                          int nslot, const HxtRole& ro, char* obase, int64_t pstride, int64_t aCol,
+                                          int64_t oRow0, bool colOk, int ccol, bool fullRb) {
+    const int sh = -(x.ea + kHxXs);
+    const int GQ = x.G * x.Qc;
+    const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
+    const uint32_t pst = 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(ro.st);
+    const int dbg = kHxsDev ? x.dbg : 0;
+    auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
+        const f32x4 y = hxScale(oA, oL, sh);
+        if (dbg & 2) return;
+        if constexpr (FAST) {
+            hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride, y, lane);
+        } else {
+            const int64_t a = aCol + p;
+            const int64_t o0 = a * x.Pc + oRow0;
+            const bool live = colOk && a < x.a_hi;
+            if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+                char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
+                hxsStoreFast<VST>(x, pp, y, lane);
+            } else if (live) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t o = o0 + i;
+                    if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi)
+                        *reinterpret_cast<float*>(x.out + o * x.out_fs + ccol * x.out_cs) = y[i];
+                }
+            }
+        }
+    };
+    int first = ro.ph;  // first period of group 0 with p % st == ph
+    for (int g = 0; g < x.ngroups; ++g) {
+        const int p0 = g * x.G;
+        const int pend = min(p0 + x.G, x.Np);
+        while (first < p0) first += ro.st;
+        const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
+        if (n > 0) {
+            hxtWait(sy.ld, kHxtLoaders, P + g);  // loads 0 .. P+g-1: stage 0 and stages 1 .. g in the ring
+            // the lane's ring offset, recomputed per group (a value held across the group loop spills,
+            // and its reload's vmcnt(0) would wait for this wave's output stores)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            const uint32_t lo = ((ln & 15) & 3) * sh_.QS + 8u * (4 * (ln >> 4) + ((ln & 15) >> 2));
+            uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(sh_.ring))) + lo + 8u * static_cast<uint32_t>(u0) +
+                          8u * static_cast<uint32_t>((g % nslot) * GQ) + 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(first - p0);
+            h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
+            for (int i = 0; i < n; ++i) {
+                asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
+                const bool last = i + 1 == n;
+                const uint32_t aL = aH + dL, aN = aH + pst, aNL = aN + dL;
+                f32x4 nA = {0, 0, 0, 0}, nL = nA;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const int ug = (s + 1) / NS, us = (s + 1) % NS;
+                    h8v bhn = bh0, bln = bl0;
+                    if (!(ug == 1 && last)) {
+                        bhn = bFragA((ug == 0 ? aH : aN) + 256 * us);
+                        bln = bFragA((ug == 0 ? aL : aNL) + 256 * us);
+                    }
+                    if (!(dbg & 4)) {
+                        nA = mfma16(Ah[s], bh0, nA);
+                        nA = mfma16(Al[s], bh0, nA);
+                        nL = mfma16(Ah[s], bl0, nL);
+                    }
+                    bh0 = bhn;
+                    bl0 = bln;
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                epilogue(nA, nL, first + i * ro.st);
+                aH = aN;
+            }
+        }
+        hxtPublish(sy.cp + wt, g + 1, lane);  // this wave's reads of group g's window are done
+    }
+}
+
+template <int NS, int VST>
+__device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int b, int wt,
+                                           int lane) {
+    // A of the wave's row block (kept in registers only inside this role: the loaders' registers
+    // are the load buffers)
+    const HxtRole ro = hxtRole(x, wt);
+    const int* pt = x.progs + kBgProgInts * ro.rb;
+    const int u0 = uni(pt[4]), rbw = uni(pt[3]);
+    h8v Ah[NS], Al[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        Ah[i] = x.A[((static_cast<size_t>(ro.rb) * NS + i) * 2 + 0) * 64 + lane];
+        Al[i] = x.A[((static_cast<size_t>(ro.rb) * NS + i) * 2 + 1) * 64 + lane];
+    }
+    const uint32_t QS = sh_.QS;
+    const int GQ = x.G * x.Qc;
+    const int grp = lane >> 4, l16 = lane & 15;
+    const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+    const bool fullRb = (rbw + 1) * 16 <= x.Pc;
+    const int nslot = x.R / GQ;
+    const int P = (x.Wg + GQ - 1) / GQ;
+    const int64_t pstride = static_cast<int64_t>(x.Pc) * x.out_fs;
+    const int col = b * 16 + l16;
+    const bool colOk = col < x.ncols;
+    const int kcol = col / x.C, ccol = col - kcol * x.C;
+    const int64_t aCol = x.a_lo + static_cast<int64_t>(kcol) * x.Np;
+    const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;  // first row of this lane's accumulator
+    const bool laneFast = fullRb && colOk && aCol + x.Np <= x.a_hi && aCol * x.Pc >= x.o_lo &&
+                          (aCol + x.Np) * x.Pc <= x.o_hi;
+    char* obase = x.out + (aCol * x.Pc + oRow0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs +
+                  (VST == 2 ? 0 : ccol * x.out_cs);
+    if (__builtin_amdgcn_ballot_w64(!laneFast) == 0)
+        hxtGroups<NS, VST, true>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
+                                 colOk, ccol, fullRb);
+    else
+        hxtGroups<NS, VST, false>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
+                                  colOk, ccol, fullRb);
+}
+
+// FMT: 1 stereo f32 frames, 2 rows of 16 f32 channels.  VST: 0 any f32 layout, 1 channel-contiguous
+// f32, 2 stereo-interleaved f32 (hxsStoreFast).
+template <int NS, int FMT, int VST>
+__global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    HxsShared s;
+    s.stamp = nullptr;
+    s.QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
+    s.ring = reinterpret_cast<char*>(smem);
+    s.loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(s.QS));  // 16-B aligned (QS % 16 == 0)
+    s.loudHi = s.loudLo + 16;
+    s.flag = s.loudHi + 16;
+    HxtSync sy;
+    // 160 B past loudLo: ld[4], cp[12] (hxsLds reserves 256 B past the ring)
+    sy.ld = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + 160);
+    sy.cp = sy.ld + 4;
+    const int lane = threadIdx.x & 63;
+    const int wt = uni(threadIdx.x >> 6);
+    const bool comp = wt < x.ncomp;
+    for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
+        const int b = hxsBlock(x, bi);
+        __syncthreads();  // the previous block's ring reads and fixup done
+        if (threadIdx.x < 16) {
+            s.loudLo[threadIdx.x] = INT_MAX;
+            s.loudHi[threadIdx.x] = -1;
+            // ld[0..3], cp[0..11]; slots past the compute waves never hold back a wait
+            sy.ld[threadIdx.x] = threadIdx.x >= kHxtLoaders + x.ncomp ? INT_MAX : 0;
+        }
+        if (threadIdx.x == 16) *s.flag = 0;
+        __syncthreads();
+        if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane);
+        else hxtLoaders<FMT>(x, s, sy, b, wt - x.ncomp, lane);
+        __syncthreads();  // every wave's part of the block done; flag final
+        if (*s.flag) {  // uniform
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
+            __syncthreads();
+            hxsFixup(hxsCold(), b, s.loudLo, s.loudHi);
+        }
+    }
+    if (x.hn > 0) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
+                              static_cast<int64_t>(gridDim.x) * blockDim.x);
+}
+
+template <int NS, int FMT, int VST>
+hipError_t hxtLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxt_kernel<NS, FMT, VST>)) < lds) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL((hxt_kernel<NS, FMT, VST>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(64 * (x.ncomp + kHxtLoaders)), lds, st, x);
+    return hipGetLastError();
+}
+
+#define GAR_HXT_FOR3(M, NS) M(NS, 1, 2) M(NS, 2, 0) M(NS, 2, 1)
+#if GAR_HXS_QUICK
+#define GAR_HXT_FOR_A(M) GAR_HXT_FOR3(M, 9)
+#define GAR_HXT_FOR_B(M) GAR_HXT_FOR3(M, 10)
+#else
+#define GAR_HXT_FOR_A(M) GAR_HXT_FOR3(M, 1) GAR_HXT_FOR3(M, 2) GAR_HXT_FOR3(M, 3) GAR_HXT_FOR3(M, 4) GAR_HXT_FOR3(M, 5) \
+    GAR_HXT_FOR3(M, 6) GAR_HXT_FOR3(M, 7)
+#define GAR_HXT_FOR_B(M) GAR_HXT_FOR3(M, 8) GAR_HXT_FOR3(M, 9) GAR_HXT_FOR3(M, 10)
+#endif
+#define GAR_HXT_INST(NS, F, V) template hipError_t hxtLaunch<NS, F, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+
+}  // namespace gar

@@ -22,19 +22,34 @@
 #include <type_traits>
 #include <utility>
 
+#include <map>
+
 #include "gar_bg.hpp"
 #include "gar_kernels.hpp"
 
 namespace gar {
 
-void setMaxLdsOnce(const void* fn) {
+// Raises the kernel's dynamic-LDS limit to what the CU leaves next to its static LDS (160 KiB -
+// static; asking for 160 KiB with static LDS present fails, and a launch above the default limit
+// then fails with "invalid argument").  Returns the dynamic-LDS limit in force (bytes).
+size_t setMaxLdsOnce(const void* fn) {
     static std::mutex mu;
-    static std::set<std::pair<int, const void*>> done;
+    static std::map<std::pair<int, const void*>, size_t> done;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
     std::lock_guard<std::mutex> lk(mu);
-    if (!done.insert({dev, fn}).second) return;
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    auto it = done.find({dev, fn});
+    if (it != done.end()) return it->second;
+    hipFuncAttributes fa{};
+    size_t lim = 0;
+    if (hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.sharedSizeBytes <= 160 * 1024) {
+        const size_t want = 160 * 1024 - fa.sharedSizeBytes;
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(want)) == hipSuccess) lim = want;
+    }
+    (void)hipGetLastError();
+    if (lim == 0) lim = 64 * 1024 > fa.sharedSizeBytes ? 64 * 1024 - fa.sharedSizeBytes : 0;  // the default limit
+    done[{dev, fn}] = lim;
+    return lim;
 }
 
 hipError_t bgLaunchF32a(int NS, const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
@@ -91,6 +106,16 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
             g.ht0 = hc->t0;
             g.hn = hc->n;
             hc->done = true;
+        }
+        // time-major (bg_rt_kernel, knob GAR_BG_RT=0: bg_rb_kernel): workgroups = row blocks x channels
+        // x blocks of 16 consecutive macro periods, each window staged once in LDS
+        static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : 0;
+        const size_t rtLds = bgRtLds(p.Qc, p.Kread, p.maxPrb, 8);
+        if (knobRt && rtLds <= 64 * 1024) {
+            g.rbMode = 2;
+            const int64_t nkb = (nmac + 15) / 16;
+            const int64_t blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);
+            return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, rtLds, blocks, stream, false);
         }
         const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
         return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, 0, blocks, stream, false);
