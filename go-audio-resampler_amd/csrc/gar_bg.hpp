@@ -685,6 +685,108 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
     if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
 }
 
+// Small launches of row-block-aligned plans, column blocks as bg_rb_kernel (16 consecutive columns,
+// column = chunk * C + channel) but each workgroup stages its block's union window -- rows
+// [first chunk's window start, last chunk's window end) x the block's channels -- once in LDS,
+// row-major ([row][channel]), so the staging loads of an interleaved stream are contiguous
+// (GAR_BG_RT=2).  Same programs, same sums as bg_kernel / bg_rb_kernel.
+__host__ __device__ inline void bgRcGeom(int64_t C, int Qc, int Kread, int& rows, int& width) {
+    // the widest block: 16 columns spanning the most chunks (C < 16) or 16 channels (C >= 16)
+    const int64_t chunks = C >= 16 ? 2 : (15 + C - 1) / C + 1;
+    rows = static_cast<int>((chunks - 1) * Qc + Kread);
+    width = static_cast<int>(C >= 16 ? 16 : C);
+}
+inline size_t bgRcLds(int64_t C, int Qc, int Kread, int nprog, size_t esz) {
+    int rows, width;
+    bgRcGeom(C, Qc, Kread, rows, width);
+    return (static_cast<size_t>(rows) * (width + 1) * esz + 15) / 16 * 16 + static_cast<size_t>(nprog) * 64 * 4 * esz;
+}
+
+template <class TC, int NS>
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rc_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+    typedef typename Acc<TC>::V V;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wt = threadIdx.x >> 6;
+    const TC* Aimg = static_cast<const TC*>(p.A);
+    int rowsMax, width;
+    bgRcGeom(g.C, g.Qc, g.Wl, rowsMax, width);
+    const int ws = width + 1;  // padded row: the 16 columns of a B read spread over the banks
+    TC* win = reinterpret_cast<TC*>(smem);
+    V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(rowsMax) * ws * sizeof(TC) + 15) / 16 * 16);
+    const int nv = g.nblocks * p.nrb;
+    const bool same = srcSameType<TC>(src);
+    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
+        const int b = v / p.nrb, rb = v - b * p.nrb;
+        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
+        TC A[NS];
+        int k0 = 0;
+        if (wt < np) {  // A lands while the window is staged
+            const int pr = ps + wt;
+            k0 = g.rbK0[pr];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+        }
+        const int col0 = b * 16, kf = col0 / g.C;
+        const int c0 = g.C >= 16 ? col0 - kf * g.C : 0;  // first channel of the block (C >= 16), else 0
+        const int kl = min(col0 + 15, g.ncols - 1) / g.C;
+        const int nrow = (kl - kf) * g.Qc + g.Wl;
+        const int64_t T = (g.a_lo + kf) * g.Qc;
+        const int nel = nrow * width;
+        for (int e0 = threadIdx.x; e0 < nel; e0 += 4 * blockDim.x) {
+            TC vv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = e0 + u * blockDim.x;
+                const int r = e / width, ch = e - r * width;
+                const int c = c0 + ch;
+                const bool ok = e < nel && c < g.C;
+                vv[u] = same ? srcReadBF<TC>(src, T + r, ok ? c : 0, ok, Aimg) : (ok ? srcRead<TC>(src, T + r, c) : TC(0));
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = e0 + u * blockDim.x;
+                const int r = e / width, ch = e - r * width;
+                if (e < nel) win[r * ws + ch] = vv[u];
+            }
+        }
+        if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside the staging
+        __syncthreads();  // window staged
+        const int col = col0 + (lane & 15), kq = lane >> 4;
+        const bool colOk = col < g.ncols;
+        const int kc = colOk ? col / g.C : kf, c = colOk ? col - kc * g.C : c0;
+        const int64_t a = g.a_lo + kc;
+        V r = {0, 0, 0, 0};
+        if (wt < np) {
+            const int base = ((kc - kf) * g.Qc + k0 + kq) * ws + (c - c0);
+            TC B[NS];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) B[s] = win[base + 4 * s * ws];
+            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+            }
+            r = acc0 + acc1;
+            if (np > 1) slots[wt * 64 + lane] = r;
+        }
+        if (np > 1) {
+            __syncthreads();
+            if (wt == 0) {
+                V sum = slots[lane];
+                for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
+                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            }
+        } else if (wt == 0 && !(g.dbg & 2)) {
+            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        }
+        __syncthreads();  // window and slots free for the next (column block, row block)
+    }
+    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;
+    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);
+}
+
 template <class TC, int NS>
 static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                              size_t lds, int64_t blocks, hipStream_t st, bool globalB) {
@@ -699,6 +801,9 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
             if (g.rbMode == 2) {  // time-major, LDS-staged windows
                 if (setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)) < lds) return hipErrorOutOfMemory;
                 hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
+            } else if (g.rbMode == 3) {  // column blocks, row-major LDS-staged windows
+                if (setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rc_kernel<TC, NS>)) < lds) return hipErrorOutOfMemory;
+                hipLaunchKernelGGL((bg_rc_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
             } else {
                 hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
             }

@@ -17,7 +17,7 @@ namespace gar {
 GAR_HXS_FOR_ALL(GAR_HXS_EXT)
 #undef GAR_HXS_EXT
 // hxt_kernel instantiations: gar_hxt_i1.hip / gar_hxt_i2.hip
-#define GAR_HXT_EXT(NS, F, V) extern template hipError_t hxtLaunch<NS, F, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+#define GAR_HXT_EXT(NS, F, V, L) extern template hipError_t hxtLaunch<NS, F, V, L>(const HxsArgs&, size_t, int64_t, hipStream_t);
 GAR_HXT_FOR_A(GAR_HXT_EXT)
 GAR_HXT_FOR_B(GAR_HXT_EXT)
 #undef GAR_HXT_EXT
@@ -77,12 +77,16 @@ unsigned long long* profBuf() {
 int64_t fdiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
 
+template <int NS, int NL>
+hipError_t hxtFmtL(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    if (x.fmt == 1 && x.vst == 2) return hxtLaunch<NS, 1, 2, NL>(x, lds, blocks, st);
+    if (x.fmt == 2 && x.vst == 0) return hxtLaunch<NS, 2, 0, NL>(x, lds, blocks, st);
+    if (x.fmt == 2 && x.vst == 1) return hxtLaunch<NS, 2, 1, NL>(x, lds, blocks, st);
+    return hipErrorNotSupported;
+}
 template <int NS>
 hipError_t hxtFmt(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
-    if (x.fmt == 1 && x.vst == 2) return hxtLaunch<NS, 1, 2>(x, lds, blocks, st);
-    if (x.fmt == 2 && x.vst == 0) return hxtLaunch<NS, 2, 0>(x, lds, blocks, st);
-    if (x.fmt == 2 && x.vst == 1) return hxtLaunch<NS, 2, 1>(x, lds, blocks, st);
-    return hipErrorNotSupported;
+    return x.ncomp + 6 <= kHxtWaves ? hxtFmtL<NS, 6>(x, lds, blocks, st) : hxtFmtL<NS, 4>(x, lds, blocks, st);
 }
 
 // Compute-wave roles of hxt_kernel for nprog row blocks (HxsArgs::role): the first 4*floor(nprog/4)
@@ -90,9 +94,14 @@ hipError_t hxtFmt(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 // 2 waves each (every 2nd period), so waves w, w+4, w+8 -- one SIMD -- carry equal MFMA work.
 // Returns the compute wave count; *maxStride the largest period stride.
 static int hxtRoles(int nprog, int* role, int* maxStride) {
-    const int q = nprog / 4 * 4, r = nprog - q;
+    static const int knobRoles = std::getenv("GAR_HXT_ROLES") ? std::atoi(std::getenv("GAR_HXT_ROLES")) : 1;
     int w = 0;
     *maxStride = 1;
+    if (!knobRoles) {  // one wave per row block (hxs_kernel's mapping), six loaders beside ten compute waves
+        for (int i = 0; i < nprog; ++i) role[w++] = i | (1 << 16);
+        return w;
+    }
+    const int q = nprog / 4 * 4, r = nprog - q;
     for (int i = 0; i < q; ++i) role[w++] = i | (1 << 16);
     if (r == 2 && q + 4 <= kHxtMaxComp) {
         for (int i = 0; i < 4; ++i) role[w++] = (q + (i & 1)) | ((i >> 1) << 8) | (2 << 16);
@@ -214,9 +223,12 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     else vst = 0;
 
     // balanced kernel (hxt_kernel): f32 stereo frames or 16-channel rows in, f32 out (knob GAR_HXT=0: hxs_kernel)
-    static const int knobHxt = std::getenv("GAR_HXT") ? std::atoi(std::getenv("GAR_HXT")) : 0;
+    // Default (knob unset): hxt_kernel for NS >= 10, where hxs_kernel's compute waves hold A (80 VGPRs)
+    // beside double-buffered accumulators and spill (cfg3 48k->44.1k Q32: 0.48 -> 0.36 ms); hxs_kernel
+    // below, where it is still the faster of the two (cfg2 / ns256, NS = 9).
+    static const int knobHxt = std::getenv("GAR_HXT") ? std::atoi(std::getenv("GAR_HXT")) : -1;
     int role[kHxtMaxComp] = {}, maxStride = 1, ncomp = 0;
-    const bool hxt = knobHxt && !small && !od.pcm && !od.f64 && !src.in_pcm &&
+    const bool hxt = (knobHxt > 0 || (knobHxt < 0 && p.NS >= 10)) && !small && !od.pcm && !od.f64 && !src.in_pcm &&
                      ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
     if (hxt) ncomp = hxtRoles(p.nw, role, &maxStride);
 

@@ -884,6 +884,23 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
     const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
     const int sh = -(x.ea + kHxXs);
+    // history keep for the next call: the first kHk elements of this thread are read up front, so
+    // their round trip overlaps the window gather's instead of following the MFMAs
+    constexpr int kHk = 2;
+    const int64_t hme = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t hnth = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t htot = x.hn * x.C;
+    float hk[kHk];
+    if (x.hn > 0) {
+        const HxsArgsP xc = hxsCold();
+        const SrcDesc src = kload(&xc->src);
+#pragma unroll
+        for (int u = 0; u < kHk; ++u) {
+            const int64_t i = hme + u * hnth;
+            const int64_t t = i / x.C;
+            hk[u] = i < htot ? hxsGather(src, x.ht0 + t, static_cast<int>(i - t * x.C), x.A) : 0.f;
+        }
+    }
     for (int b = blockIdx.x; b < x.nblocks; b += gridDim.x) {
         if (threadIdx.x < 16) { loudLo[threadIdx.x] = INT_MAX; loudHi[threadIdx.x] = -1; }
         if (threadIdx.x == 0) *flag = 0;
@@ -934,8 +951,12 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
         }
         __syncthreads();  // every wave done with the image / loud state before the next block
     }
-    if (x.hn > 0) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
-                              static_cast<int64_t>(gridDim.x) * blockDim.x);
+    if (x.hn > 0) {
+#pragma unroll
+        for (int u = 0; u < kHk; ++u)
+            if (hme + u * hnth < htot) x.hdst[hme + u * hnth] = hk[u];
+        if (htot > kHk * hnth) hxsHistKeep(x, hme + kHk * hnth, hnth);  // the rest (long histories)
+    }
 }
 
 template <int NS, int VST>

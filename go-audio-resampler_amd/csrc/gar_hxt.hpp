@@ -26,13 +26,17 @@
 
 namespace gar {
 
-constexpr int kHxtLoaders = 4;                          // one loader wave per SIMD
+// NL loader waves (template parameter, 4 or 6) + up to 16 - NL compute waves, 16 waves at most.
 constexpr int kHxtMaxComp = 12;                         // compute waves (3 per SIMD)
-constexpr int kHxtWaves = kHxtMaxComp + kHxtLoaders;    // __launch_bounds__: 16 waves, 128 VGPRs
+constexpr int kHxtWaves = 16;                           // __launch_bounds__: 16 waves, 128 VGPRs
 constexpr int kHxtD = 2;                                // loads in flight per loader (register staging)
-constexpr int kHxtItems = 10;                           // items per loader per load
-constexpr int kHxtMaxRows = 64 * kHxtItems;             // rows of one load (G*Qc): FMT 1 quad l = loader l,
-                                                        // 64-row pieces; FMT 2 16-row pieces l, l+4, ...
+constexpr int kHxtPieces = 10;                          // 64-row pieces of one load
+constexpr int kHxtMaxRows = 64 * kHxtPieces;            // rows of one load (G*Qc)
+// Items of loader l (of NL): FMT 1 item it = l + NL*k covers quad it & 3, 64-row piece it >> 2;
+// FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row).
+template <int NL>
+constexpr int hxtItems() { return (4 * kHxtPieces + NL - 1) / NL; }
+constexpr int kHxtLdSlots = 8;                          // progress counters: ld[8] (loaders), cp[12] (compute)
 constexpr uint32_t kHxtLoudBits = 0x41800000u;          // bits(16.0f): |x| >= 16, Inf, NaN <=> (bits & 0x7fffffff) >= it
 
 struct HxtRole {
@@ -44,35 +48,36 @@ __device__ __forceinline__ HxtRole hxtRole(const HxsArgs& x, int w) {
 }
 
 // ---- loaders ------------------------------------------------------------------------
-template <int FMT>
+template <int FMT, int NL>
 struct HxtBuf;
-template <>
-struct HxtBuf<1> {  // stereo f32 frames: two chunks (both channels each) per item
-    f2v a[kHxtItems], b[kHxtItems];
+template <int NL>
+struct HxtBuf<1, NL> {  // stereo f32 frames: two chunks (both channels each) per item
+    f2v a[hxtItems<NL>()], b[hxtItems<NL>()];
 };
-template <>
-struct HxtBuf<2> {  // 16-channel f32 rows: four channels of one row per lane
-    f32x4 v[kHxtItems];
+template <int NL>
+struct HxtBuf<2, NL> {  // 16-channel f32 rows: four channels of one row per lane
+    f32x4 v[hxtItems<NL>()];
 };
 
 // Issue load `st` (a real load when live and fast; otherwise every item's offset lies past the
 // records, which returns zeros without a memory access -- the same instruction pattern on every
 // path, so the compiler's vmcnt tracking waits for exactly the oldest load).
-template <int FMT>
-__device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxtBuf<FMT>& r) {
+template <int FMT, int NL>
+__device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxtBuf<FMT, NL>& r) {
     const bool fast = live && st.fast;
     const int nrow = fast ? st.nrow : 0;
     const int base = st.T0 * rs.rowB + rs.lane0;
 #pragma unroll
-    for (int k = 0; k < kHxtItems; ++k) {
-        if constexpr (FMT == 1) {  // quad l = chunks 2l, 2l+1; piece k = rows 64k ..
-            const bool on = 64 * k < nrow;
-            const int o = on ? base + 64 * k * rs.rowB + 2 * l * rs.chunkB : static_cast<int>(0x80000000u);
+    for (int k = 0; k < hxtItems<NL>(); ++k) {
+        if constexpr (FMT == 1) {  // item it: quad q = chunks 2q, 2q+1; piece it >> 2 = rows 64 (it >> 2) ..
+            const int it = l + NL * k, q = it & 3, pc = it >> 2;
+            const bool on = pc < kHxtPieces && 64 * pc < nrow;
+            const int o = on ? base + 64 * pc * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
             const int o2 = on ? o + rs.chunkB : o;
             r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
             r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
-        } else {  // 16-row piece l + 4k, lane = 16 quad + row
-            const int it = l + kHxtLoaders * k;
+        } else {  // 16-row piece l + NL k, lane = 16 quad + row
+            const int it = l + NL * k;
             const bool on = 16 * it < nrow;
             const int o = on ? base + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
             r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
@@ -96,8 +101,8 @@ __device__ __forceinline__ void hxtPut(char* qb, uint32_t dL, int p, int R, int 
 
 __device__ __forceinline__ uint32_t hxtMag(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
-template <int FMT>
-__device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT>& r, int k) {
+template <int FMT, int NL>
+__device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT, NL>& r, int k) {
     if constexpr (FMT == 1) return f32x4{r.a[k].x, r.a[k].y, r.b[k].x, r.b[k].y};
     else return r.v[k];
 }
@@ -105,18 +110,19 @@ __device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT>& r, int k) {
 // Exact per-element path of a load that holds a loud element (rare, out of line): loader l's items
 // of the load again, re-read from memory through the SrcDesc with the fast path's item mapping and
 // staged through hxsPutItem (loud elements as zero, their column rows recorded).
-template <int FMT>
+template <int FMT, int NL>
 __device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
     const SrcDesc src = kload(&xp->src);
     const int p0 = uni(st.T0 % xp->R);
-    for (int k = 0; k < kHxtItems; ++k) {
+    for (int k = 0; k < hxtItems<NL>(); ++k) {
         int row, q;
         if constexpr (FMT == 1) {
-            if (64 * k >= st.nrow) break;
-            row = 64 * k + lane;
-            q = l;
+            const int it = l + NL * k, pc = it >> 2;
+            if (pc >= kHxtPieces || 64 * pc >= st.nrow) continue;
+            row = 64 * pc + lane;
+            q = it & 3;
         } else {
-            const int it = l + kHxtLoaders * k;
+            const int it = l + NL * k;
             if (16 * it >= st.nrow) break;
             row = 16 * it + (lane & 15);
             q = lane >> 4;
@@ -136,11 +142,11 @@ __device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l,
 // Edge load (rows before the raw input, partial blocks, any other layout): every element gathered
 // through the SrcDesc (history | input | zeros); out of line.  Loader l takes items l, l+4, ...
 // of the 4 quads x ceil(nrow/64) pieces.
-__device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
+__device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int nl, int lane, HxsShared sh) {
     const SrcDesc src = kload(&xp->src);
     const int p0 = uni(st.T0 % xp->R);
     const int nit = 4 * ((st.nrow + 63) >> 6);
-    for (int it = l; it < nit; it += kHxtLoaders) {
+    for (int it = l; it < nit; it += nl) {
         const int q = it & 3, row = 64 * (it >> 2) + lane;
         if (row >= st.nrow) continue;
         f32x4 e;
@@ -155,8 +161,8 @@ __device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int 
 }
 
 // Fast load `st` -> ring (registers of its issue): split, write, one running max for the loud test.
-template <int FMT>
-__device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, const HxtBuf<FMT>& r, int b, int l,
+template <int FMT, int NL>
+__device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, const HxtBuf<FMT, NL>& r, int b, int l,
                                            int lane, const HxsShared& sh) {
     const int R = x.R, mirror = x.mirror;
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
@@ -168,21 +174,22 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
     asm volatile("" : "+v"(ln));
     uint32_t m = 0;
 #pragma unroll
-    for (int k = 0; k < kHxtItems; ++k) {
+    for (int k = 0; k < hxtItems<NL>(); ++k) {
         int row, q;
         bool on;
         if constexpr (FMT == 1) {
-            on = 64 * k < nrow;
-            row = 64 * k + ln;
-            q = l;
+            const int it = l + NL * k, pc = it >> 2;
+            on = pc < kHxtPieces && 64 * pc < nrow;
+            row = 64 * pc + ln;
+            q = it & 3;
         } else {
-            const int it = l + kHxtLoaders * k;
+            const int it = l + NL * k;
             on = 16 * it < nrow;
             row = 16 * it + (ln & 15);
             q = ln >> 4;
         }
         if (on) {  // uniform
-            const f32x4 e = hxtItem<FMT>(r, k);
+            const f32x4 e = hxtItem<FMT, NL>(r, k);
             m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
             int p = p0 + row;
             p = p >= R ? p - R : p;
@@ -190,7 +197,7 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
         }
     }
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
-        hxtLoudLoad<FMT>(hxsCold(), st, b, l, lane, sh);
+        hxtLoudLoad<FMT, NL>(hxsCold(), st, b, l, lane, sh);
 }
 
 // ---- progress counters (LDS) -------------------------------------------------------------
@@ -207,7 +214,7 @@ typedef __attribute__((address_space(3))) i32x4v lds_i32x4;
 // Explicit LDS pointers: a generic pointer makes the polls flat loads, and a flat load's
 // s_waitcnt vmcnt(0) waits for every store the wave has in flight.
 struct HxtSync {
-    lds_i32* ld;  // [kHxtLoaders]
+    lds_i32* ld;  // [kHxtLdSlots]
     lds_i32* cp;  // [kHxtMaxComp]
 };
 
@@ -249,7 +256,7 @@ __device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
 // Loader wave l: in step j it waits for the ring rows of load j to be free, converts load j
 // (issued kHxtD steps earlier) into the ring, publishes it and issues load j + kHxtD into the
 // registers just freed.
-template <int FMT>
+template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
                                            int lane) {
     const HxsArgsP xp = hxsCold();
@@ -257,11 +264,11 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
     const int nstepsPad = hxsStepsPad(x);
     const int dbg = kHxsDev ? x.dbg : 0;
-    HxtBuf<FMT> buf[kHxtD];
+    HxtBuf<FMT, NL> buf[kHxtD];
     bool fastL[kHxtD];
     const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
 #pragma unroll
-    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT>(hxsLoad(xp, b, d, P), d < nL, rs, l, buf[d]);
+    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(hxsLoad(xp, b, d, P), d < nL, rs, l, buf[d]);
     for (int j0 = 0; j0 < nstepsPad; j0 += kHxtD) {
 #pragma unroll
         for (int d = 0; d < kHxtD; ++d) {
@@ -270,12 +277,12 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (j >= P) hxtWait(sy.cp, x.ncomp, hxtFreeNeed(x, j, P));
                 if (!((dbg & 16) && j >= P)) {
                     const HxsStage st = hxsLoad(xp, b, j, P);
-                    if (fastL[d]) hxtConvert<FMT>(x, st, buf[d], b, l, lane, sh);
-                    else hxtGatherLoad(xp, st, b, l, lane, sh);
+                    if (fastL[d]) hxtConvert<FMT, NL>(x, st, buf[d], b, l, lane, sh);
+                    else hxtGatherLoad(xp, st, b, l, NL, lane, sh);
                 }
                 hxtPublish(sy.ld + l, j + 1, lane);
             }
-            fastL[d] = hxtIssue<FMT>(hxsLoad(xp, b, j + kHxtD, P), j + kHxtD < nL && !((dbg & 1) && j >= P), rs, l,
+            fastL[d] = hxtIssue<FMT, NL>(hxsLoad(xp, b, j + kHxtD, P), j + kHxtD < nL && !((dbg & 1) && j >= P), rs, l,
                                      buf[d]);
         }
     }
@@ -324,7 +331,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         while (first < p0) first += ro.st;
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
-            hxtWait(sy.ld, kHxtLoaders, P + g);  // loads 0 .. P+g-1: stage 0 and stages 1 .. g in the ring
+            hxtWait(sy.ld, kHxtLdSlots, P + g);  // loads 0 .. P+g-1: stage 0 and stages 1 .. g in the ring
             // the lane's ring offset, recomputed per group (a value held across the group loop spills,
             // and its reload's vmcnt(0) would wait for this wave's output stores)
             int ln = lane;
@@ -406,7 +413,7 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
 
 // FMT: 1 stereo f32 frames, 2 rows of 16 f32 channels.  VST: 0 any f32 layout, 1 channel-contiguous
 // f32, 2 stereo-interleaved f32 (hxsStoreFast).
-template <int NS, int FMT, int VST>
+template <int NS, int FMT, int VST, int NL>
 __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     HxsShared s;
@@ -417,9 +424,9 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     s.loudHi = s.loudLo + 16;
     s.flag = s.loudHi + 16;
     HxtSync sy;
-    // 160 B past loudLo: ld[4], cp[12] (hxsLds reserves 256 B past the ring)
+    // 160 B past loudLo: ld[8], cp[12] (hxsLds reserves 256 B past the ring)
     sy.ld = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + 160);
-    sy.cp = sy.ld + 4;
+    sy.cp = sy.ld + kHxtLdSlots;
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
     const bool comp = wt < x.ncomp;
@@ -429,13 +436,15 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
         if (threadIdx.x < 16) {
             s.loudLo[threadIdx.x] = INT_MAX;
             s.loudHi[threadIdx.x] = -1;
-            // ld[0..3], cp[0..11]; slots past the compute waves never hold back a wait
-            sy.ld[threadIdx.x] = threadIdx.x >= kHxtLoaders + x.ncomp ? INT_MAX : 0;
+        }
+        if (threadIdx.x < kHxtLdSlots + kHxtMaxComp) {  // ld[8], cp[12]; unused slots never hold back a wait
+            const int i = threadIdx.x;
+            sy.ld[i] = (i < kHxtLdSlots ? i >= NL : i - kHxtLdSlots >= x.ncomp) ? INT_MAX : 0;
         }
         if (threadIdx.x == 16) *s.flag = 0;
         __syncthreads();
         if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane);
-        else hxtLoaders<FMT>(x, s, sy, b, wt - x.ncomp, lane);
+        else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane);
         __syncthreads();  // every wave's part of the block done; flag final
         if (*s.flag) {  // uniform
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
@@ -447,15 +456,16 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
                               static_cast<int64_t>(gridDim.x) * blockDim.x);
 }
 
-template <int NS, int FMT, int VST>
+template <int NS, int FMT, int VST, int NL>
 hipError_t hxtLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
-    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxt_kernel<NS, FMT, VST>)) < lds) return hipErrorOutOfMemory;
-    hipLaunchKernelGGL((hxt_kernel<NS, FMT, VST>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(64 * (x.ncomp + kHxtLoaders)), lds, st, x);
+    if (x.ncomp + NL > kHxtWaves) return hipErrorInvalidConfiguration;
+    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxt_kernel<NS, FMT, VST, NL>)) < lds) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL((hxt_kernel<NS, FMT, VST, NL>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.ncomp + NL)), lds,
+                       st, x);
     return hipGetLastError();
 }
 
-#define GAR_HXT_FOR3(M, NS) M(NS, 1, 2) M(NS, 2, 0) M(NS, 2, 1)
+#define GAR_HXT_FOR3(M, NS) M(NS, 1, 2, 4) M(NS, 2, 0, 4) M(NS, 2, 1, 4) M(NS, 1, 2, 6) M(NS, 2, 0, 6) M(NS, 2, 1, 6)
 #if GAR_HXS_QUICK
 #define GAR_HXT_FOR_A(M) GAR_HXT_FOR3(M, 9)
 #define GAR_HXT_FOR_B(M) GAR_HXT_FOR3(M, 10)
@@ -464,6 +474,6 @@ hipError_t hxtLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t s
     GAR_HXT_FOR3(M, 6) GAR_HXT_FOR3(M, 7)
 #define GAR_HXT_FOR_B(M) GAR_HXT_FOR3(M, 8) GAR_HXT_FOR3(M, 9) GAR_HXT_FOR3(M, 10)
 #endif
-#define GAR_HXT_INST(NS, F, V) template hipError_t hxtLaunch<NS, F, V>(const HxsArgs&, size_t, int64_t, hipStream_t);
+#define GAR_HXT_INST(NS, F, V, L) template hipError_t hxtLaunch<NS, F, V, L>(const HxsArgs&, size_t, int64_t, hipStream_t);
 
 }  // namespace gar

@@ -111,11 +111,17 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
         // x blocks of 16 consecutive macro periods, each window staged once in LDS
         static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : 0;
         const size_t rtLds = bgRtLds(p.Qc, p.Kread, p.maxPrb, 8);
-        if (knobRt && rtLds <= 64 * 1024) {
+        if (knobRt == 1 && rtLds <= 64 * 1024) {
             g.rbMode = 2;
             const int64_t nkb = (nmac + 15) / 16;
             const int64_t blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);
             return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, rtLds, blocks, stream, false);
+        }
+        const size_t rcLds = bgRcLds(C, p.Qc, p.Kread, p.maxPrb, 8);
+        if (knobRt == 2 && rcLds <= 160 * 1024 - 1024) {
+            g.rbMode = 3;
+            const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
+            return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, rcLds, blocks, stream, false);
         }
         const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
         return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, 0, blocks, stream, false);
