@@ -240,7 +240,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
             if (cand > 1 && cand > Np) continue;
             if (knobG > 0 && cand > knobG && cand > 1) continue;
             if (!hxsRingFits(p, cand, rt)) continue;
-            if (hxt && cand * Qc > kHxtMaxRows) continue;
+            if (hxt && cand * Qc > hxtMaxRows(ncomp + 6 <= kHxtWaves ? 6 : 4)) continue;
             if (pass == 0 && cand % maxStride != 0) continue;
             G = cand; R = r; Rt = rt; Wg = wg;
             break;

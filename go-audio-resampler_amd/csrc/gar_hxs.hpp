@@ -420,6 +420,60 @@ __device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const
     return fast;
 }
 
+// Small launches, interior blocks of a STEREO (fmt 1) / ROW16 (fmt 2) f32 input: the window [0, Wg)
+// of every column comes straight from the raw input through buffer loads -- one 8-B load (both
+// channels of a chunk) or one 16-B load (four channels) per lane and row, rows past the input end
+// read as zeros through the records -- instead of four branch-free scalar gathers per item, whose
+// 64-bit address arithmetic dominated a short call's instruction stream.  Same image, same split.
+template <class XP>
+__device__ __forceinline__ bool hxsSmallFast(XP x, int b, int tid, int nth, char* ring, uint32_t QS, int* loudLo,
+                                             int* loudHi, int* flag) {
+    if (x->fmt != 1 && x->fmt != 2) return false;
+    const HxsStage st = hxsStage(x, b, 0, x->Wg);  // fast: every column live, row 0 at or after the raw input
+    if (!st.fast) return false;
+    const int lane = tid & 63, w = tid >> 6, nw = nth >> 6;
+    constexpr int kB = 4;  // items per wave in flight
+    if (x->fmt == 1) {
+        const HxsRegSrc rs = hxsRegSrc<1>(x, b, lane);
+        const int nit = 4 * ((st.nrow + 63) >> 6);
+        for (int it0 = w; it0 < nit; it0 += kB * nw) {
+            f2v a[kB], c[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int it = it0 + u * nw, q = it & 3, pc = it >> 2;
+                const int o = it < nit ? rs.lane0 + 64 * pc * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
+                const int o2 = it < nit ? o + rs.chunkB : o;
+                a[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
+                c[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int it = it0 + u * nw, row = 64 * (it >> 2) + lane;
+                if (it < nit && row < st.nrow)
+                    hxsPutItem(x, st, 0, it & 3, row, f32x4{a[u].x, a[u].y, c[u].x, c[u].y}, ring, QS, loudLo, loudHi, flag);
+            }
+        }
+    } else {
+        const HxsRegSrc rs = hxsRegSrc<2>(x, b, lane);
+        const int nit = (st.nrow + 15) >> 4;
+        for (int it0 = w; it0 < nit; it0 += kB * nw) {
+            f32x4 v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int it = it0 + u * nw;
+                const int o = it < nit ? rs.lane0 + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
+                v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int it = it0 + u * nw, row = 16 * it + (lane & 15);
+                if (it < nit && row < st.nrow) hxsPutItem(x, st, 0, lane >> 4, row, v[u], ring, QS, loudLo, loudHi, flag);
+            }
+        }
+    }
+    return true;
+}
+
 // int(clamp(float64(y), -1, 1) * 32767) with pcmWrite's semantics (f64 product: exact; NaN -> 0).
 __device__ __forceinline__ int32_t pcm16Of(float y) {
     const double d = static_cast<double>(y);
@@ -905,7 +959,8 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
         if (threadIdx.x < 16) { loudLo[threadIdx.x] = INT_MAX; loudHi[threadIdx.x] = -1; }
         if (threadIdx.x == 0) *flag = 0;
         __syncthreads();  // loud state reset; the previous block's image reads done
-        hxsSmallStage(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag);
+        if (!hxsSmallFast(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag))
+            hxsSmallStage(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag);
         __syncthreads();  // the whole window in the image
         if (comp) {
             const uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) + 8u * static_cast<uint32_t>(u0);

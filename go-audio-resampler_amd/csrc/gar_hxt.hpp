@@ -30,12 +30,14 @@ namespace gar {
 constexpr int kHxtMaxComp = 12;                         // compute waves (3 per SIMD)
 constexpr int kHxtWaves = 16;                           // __launch_bounds__: 16 waves, 128 VGPRs
 constexpr int kHxtD = 2;                                // loads in flight per loader (register staging)
-constexpr int kHxtPieces = 10;                          // 64-row pieces of one load
-constexpr int kHxtMaxRows = 64 * kHxtPieces;            // rows of one load (G*Qc)
+// 64-row pieces of one load (G*Qc <= 64 * pieces): 10 with 4 loaders, 12 with 6 (the registers
+// of a loader's two loads in flight stay at 80 / 64 VGPRs)
+__host__ __device__ constexpr int hxtPieces(int NL) { return NL >= 6 ? 12 : 10; }
+__host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL); }
 // Items of loader l (of NL): FMT 1 item it = l + NL*k covers quad it & 3, 64-row piece it >> 2;
 // FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row).
 template <int NL>
-constexpr int hxtItems() { return (4 * kHxtPieces + NL - 1) / NL; }
+constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 constexpr int kHxtLdSlots = 8;                          // progress counters: ld[8] (loaders), cp[12] (compute)
 constexpr uint32_t kHxtLoudBits = 0x41800000u;          // bits(16.0f): |x| >= 16, Inf, NaN <=> (bits & 0x7fffffff) >= it
 
@@ -71,7 +73,7 @@ __device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const Hx
     for (int k = 0; k < hxtItems<NL>(); ++k) {
         if constexpr (FMT == 1) {  // item it: quad q = chunks 2q, 2q+1; piece it >> 2 = rows 64 (it >> 2) ..
             const int it = l + NL * k, q = it & 3, pc = it >> 2;
-            const bool on = pc < kHxtPieces && 64 * pc < nrow;
+            const bool on = pc < hxtPieces(NL) && 64 * pc < nrow;
             const int o = on ? base + 64 * pc * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
             const int o2 = on ? o + rs.chunkB : o;
             r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
@@ -118,7 +120,7 @@ __device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l,
         int row, q;
         if constexpr (FMT == 1) {
             const int it = l + NL * k, pc = it >> 2;
-            if (pc >= kHxtPieces || 64 * pc >= st.nrow) continue;
+            if (pc >= hxtPieces(NL) || 64 * pc >= st.nrow) continue;
             row = 64 * pc + lane;
             q = it & 3;
         } else {
@@ -162,11 +164,10 @@ __device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int 
 
 // Fast load `st` -> ring (registers of its issue): split, write, one running max for the loud test.
 template <int FMT, int NL>
-__device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, const HxtBuf<FMT, NL>& r, int b, int l,
-                                           int lane, const HxsShared& sh) {
+__device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, int p0, const HxtBuf<FMT, NL>& r, int b,
+                                           int l, int lane, const HxsShared& sh) {
     const int R = x.R, mirror = x.mirror;
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
-    const int p0 = uni(st.T0 % R);
     const int nrow = st.nrow;
     // opaque per call: the compiler must not hoist the items' row numbers out of the step loop
     // (ten live row registers spill, and every reload's vmcnt(0) waits for the loads in flight)
@@ -179,7 +180,7 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
         bool on;
         if constexpr (FMT == 1) {
             const int it = l + NL * k, pc = it >> 2;
-            on = pc < kHxtPieces && 64 * pc < nrow;
+            on = pc < hxtPieces(NL) && 64 * pc < nrow;
             row = 64 * pc + ln;
             q = it & 3;
         } else {
@@ -193,7 +194,10 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
             m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
             int p = p0 + row;
             p = p >= R ? p - R : p;
-            if (row < nrow) hxtPut(sh.ring + q * sh.QS, dL, p, R, mirror, e);
+            // quad base recomputed per item (opaque): eight hoisted per-quad bases spill to VGPR lanes
+            uint32_t qs = sh.QS;
+            asm volatile("" : "+s"(qs));
+            if (row < nrow) hxtPut(sh.ring + q * qs, dL, p, R, mirror, e);
         }
     }
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
@@ -260,30 +264,52 @@ template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
                                            int lane) {
     const HxsArgsP xp = hxsCold();
-    const int GQ = x.G * x.Qc;
-    const int P = (x.Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
+    const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
+    const int P = (Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
     const int nstepsPad = hxsStepsPad(x);
     const int dbg = kHxsDev ? x.dbg : 0;
+    // per block (uniform): loads go through the buffer records ("fast") when every column of the
+    // block is live and the load's first row lies at or after the raw input's first row
+    const int c1 = b * 16 + 15;
+    const bool blockLive = x.fmt >= 1 && x.fmt <= 4 && c1 < x.ncols && x.fastHi > x.fastLo;
+    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * 16) / x.C) * x.Np) * x.Qc;  // column-relative row 0
+    const int64_t fastLo = x.fastLo;
+    auto stage = [&](int j) {  // load j: the P parts of stage 0, then stages 1 ..
+        HxsStage st;
+        st.T0 = j < P ? j * GQ : Wg + (j - P) * GQ;
+        st.nrow = j < P ? min(GQ, Wg - j * GQ) : GQ;
+        st.fast = blockLive && row0 + st.T0 >= fastLo;
+        return st;
+    };
     HxtBuf<FMT, NL> buf[kHxtD];
     bool fastL[kHxtD];
     const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
 #pragma unroll
-    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(hxsLoad(xp, b, d, P), d < nL, rs, l, buf[d]);
+    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(d), d < nL, rs, l, buf[d]);
+    // ring row of load j's first row (incremental: T0 % R) and the groups its rows' previous
+    // occupants belong to (hxtFreeNeed, incremental)
+    int p0 = 0, last = Wg + GQ - 1 - R, need = 0;
     for (int j0 = 0; j0 < nstepsPad; j0 += kHxtD) {
 #pragma unroll
         for (int d = 0; d < kHxtD; ++d) {
             const int j = j0 + d;
             if (j < nL) {
-                if (j >= P) hxtWait(sy.cp, x.ncomp, hxtFreeNeed(x, j, P));
+                if (j >= P) {
+                    if (j == P) p0 = Wg;  // Wg < R
+                    need = last < 0 ? 0 : need + 1;
+                    if (need > 0) hxtWait(sy.cp, x.ncomp, need);
+                    last += GQ;
+                }
                 if (!((dbg & 16) && j >= P)) {
-                    const HxsStage st = hxsLoad(xp, b, j, P);
-                    if (fastL[d]) hxtConvert<FMT, NL>(x, st, buf[d], b, l, lane, sh);
+                    const HxsStage st = stage(j);
+                    if (fastL[d]) hxtConvert<FMT, NL>(x, st, uni(p0), buf[d], b, l, lane, sh);
                     else hxtGatherLoad(xp, st, b, l, NL, lane, sh);
                 }
                 hxtPublish(sy.ld + l, j + 1, lane);
+                p0 += GQ;
+                if (p0 >= R) p0 -= R;
             }
-            fastL[d] = hxtIssue<FMT, NL>(hxsLoad(xp, b, j + kHxtD, P), j + kHxtD < nL && !((dbg & 1) && j >= P), rs, l,
-                                     buf[d]);
+            fastL[d] = hxtIssue<FMT, NL>(stage(j + kHxtD), j + kHxtD < nL && !((dbg & 1) && j >= P), rs, l, buf[d]);
         }
     }
 }

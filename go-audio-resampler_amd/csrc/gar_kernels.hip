@@ -109,9 +109,12 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
         }
         // time-major (bg_rt_kernel, knob GAR_BG_RT=0: bg_rb_kernel): workgroups = row blocks x channels
         // x blocks of 16 consecutive macro periods, each window staged once in LDS
-        static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : 0;
+        // Default: time-major for plans of one or two row blocks (the integer decimator: each window is
+        // staged once; 4800-frame cfg5 calls 26.8 -> 18.9 us), bg_rb_kernel otherwise (a plan of ten row
+        // blocks would stage every window ten times: the cfg5 composite 21.8 -> 33.6 us).
+        static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : -1;
         const size_t rtLds = bgRtLds(p.Qc, p.Kread, p.maxPrb, 8);
-        if (knobRt == 1 && rtLds <= 64 * 1024) {
+        if ((knobRt == 1 || (knobRt < 0 && p.nrb <= 2)) && rtLds <= 64 * 1024) {
             g.rbMode = 2;
             const int64_t nkb = (nmac + 15) / 16;
             const int64_t blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);

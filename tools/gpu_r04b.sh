@@ -1,6 +1,8 @@
 #!/bin/bash
-# cfg5 small-launch kernels A/B (GAR_BG_RT 0 rb / 1 rt / 2 rc) with the f64 parity tests, then hxt attribution.
+# One GPU call: hxt vs hxs A/B (cfg2 ns256 cfg3), cfg5 small-launch kernels (GAR_BG_RT 0 rb / 1 rt / 2 rc)
+# with the f64 parity tests, then hxt attribution on the dev build.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/r04b; mkdir -p $O
+NO_TESTS=1 WORKLOADS="cfg2 ns256 cfg3" ABS="GAR_HXT=1 GAR_HXT=1,GAR_HXT_ROLES=0 GAR_HXT=0" bash tools/gpu_ab.sh || exit 1
 for rt in 1 2; do
   GAR_BG_RT=$rt timeout -k 10 300 python -u -m pytest -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
     tests/test_gpu_parity.py -k "f64 or cfg5 or chunking or multistage or fixture" > $O/tests_rt$rt.log 2>&1
