@@ -625,19 +625,20 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
             const int pr = ps + wt;
             k0 = g.rbK0[pr];
 #pragma unroll
-            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+            for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
         }
-        // stage rows [0, nrow) of channel c from T: batches of 4 loads per thread in flight
+        // stage rows [0, nrow) of channel c from T: batches of kRtB loads per thread in flight
         const int64_t T = (g.a_lo + 16 * static_cast<int64_t>(kb)) * Qc;
-        for (int r0 = threadIdx.x; r0 < nrow; r0 += 4 * blockDim.x) {
-            TC vv[4];
+        constexpr int kRtB = 8;  // loads per thread in flight: the decimator's ~1.7k-row window in one round trip
+        for (int r0 = threadIdx.x; r0 < nrow; r0 += kRtB * blockDim.x) {
+            TC vv[kRtB];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kRtB; ++u) {
                 const int r = r0 + u * blockDim.x;
-                vv[u] = same ? srcReadBF<TC>(src, T + r, c, r < nrow, Aimg) : (r < nrow ? srcRead<TC>(src, T + r, c) : TC(0));
+                vv[u] = (g.dbg & 16) ? TC(r) : (same ? srcReadBF<TC>(src, T + r, c, r < nrow, Aimg) : (r < nrow ? srcRead<TC>(src, T + r, c) : TC(0)));
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kRtB; ++u) {
                 const int r = r0 + u * blockDim.x;
                 if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
             }

@@ -117,6 +117,10 @@ bool attachHx(const FirPeriodic& f, StageRT::HxRT& h, BgDev& bg, bool dry, const
     d.twoStage = p.twoStage ? 1 : 0;
     d.T1 = ed.dft.taps;
     d.T2 = ed.poly.taps;
+    if (p.rbMode && p.nw <= 16) {  // hxq_kernel takes them by value
+        const std::vector<int> pt = p.progTable();
+        for (int w = 0; w < p.nw; ++w) { d.hU0[w] = pt[kBgProgInts * w + 4]; d.hRbw[w] = pt[kBgProgInts * w + 3]; }
+    }
     if (!dry) {
         h.A.upload(p.A);
         std::vector<int> t = p.progTable();

@@ -45,6 +45,9 @@ unsigned long long* profBuf() {
                                        static_cast<double>(h[20]) / h[23], static_cast<double>(h[21]) / h[23], static_cast<double>(h[22]) / h[23], h[23]);
                     if (h[23]) fprintf(stderr, "hxs wave-0: entry->A landed %.0f, entry->barrier 1 %.0f; wave entry spread in a workgroup %.0f, wave 0 after first wave %.0f\n",
                                        static_cast<double>(h[24]) / h[23], static_cast<double>(h[25]) / h[23], static_cast<double>(h[26]) / h[23], static_cast<double>(h[27]) / h[23]);
+                    if (h[44]) fprintf(stderr, "hxq wave 0 (cycles): entry->barrier 1 %.0f, ->image %.0f, ->MFMA+stores issued %.0f, ->drained %.0f, n %llu\n",
+                                       static_cast<double>(h[40]) / h[44], static_cast<double>(h[41]) / h[44], static_cast<double>(h[42]) / h[44],
+                                       static_cast<double>(h[43]) / h[44], h[44]);
                     fprintf(stderr, "hxs span: first start -> last end %.1f us; loader wave life min %.1f max %.1f us\n",
                             (h[11] - h[10]) / 100.0, h[13] / 100.0, h[14] / 100.0);
                     // per-workgroup life (last launch): percentiles, by blockIdx % 8, slowest
@@ -314,6 +317,43 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         x.hn = hc->n;
         hc->done = true;
     }
+    // small float launches: hxq_kernel over (block, row-block group) workgroups, the largest group
+    // whose launch still has a workgroup per CU (a stereo 4096-frame call: one row block per
+    // workgroup, 40 workgroups; 256 channels: all ten, 448 workgroups -- measured 18 us per call
+    // against 30 us with five).  Knobs: GAR_HXQ=0 (hxs_small_kernel), GAR_HXQ_NR (group size).
+    static const int knobHxq = std::getenv("GAR_HXQ") ? std::atoi(std::getenv("GAR_HXQ")) : 1;
+    static const int knobHxqNr = std::getenv("GAR_HXQ_NR") ? std::atoi(std::getenv("GAR_HXQ_NR")) : 0;
+    {
+        const uintptr_t hA = reinterpret_cast<uintptr_t>(src.hist);
+        const int hAl = fmt == 1 ? 8 : (fmt == 2 ? 16 : 4), hLd = fmt == 1 ? 2 : (fmt == 2 ? 4 : 1);
+        const bool histOk = !src.hist || src.hist_len <= 0 ||
+                            ((hA % hAl) == 0 && src.hist_ld % hLd == 0 && src.hist_len * src.hist_ld * 4 < (int64_t(1) << 31));
+        // any other f32 / f64 layout: per-column element loads, every offset from the block's first row < 2^31
+        const int64_t spanRows = (16 / C + 2) * Np * Qc + Wg;
+        const bool gen = fmt == 0 && !src.in_pcm && src.in_fs >= 0 && src.in_cs >= 0 &&
+                         (spanRows * src.in_fs + static_cast<int64_t>(C) * src.in_cs) * inEsz < (int64_t(1) << 31);
+        // history keep through buffer loads from row ht0: offsets < 2^31
+        const bool hkOk = !hc || hc->n <= 0 || (hc->n * src.in_fs + static_cast<int64_t>(C) * src.in_cs) * inEsz < (int64_t(1) << 31);
+        if (small && knobHxq && ((fmt == 1 || fmt == 2) ? rawSpan : gen) && histOk && hkOk && p.nw <= 12 && x.Np == 1) {
+            int nr = 1;
+            for (int cand = p.nw; cand >= 1; --cand)
+                if (x.nblocks * static_cast<int64_t>(cdiv(p.nw, cand)) >= static_cast<int64_t>(ncu)) { nr = cand; break; }
+            if (knobHxqNr > 0) nr = std::min(knobHxqNr, p.nw);
+            x.qRbs = nr;
+            x.qGroups = static_cast<int>(cdiv(p.nw, nr));
+            for (int w = 0; w < p.nw; ++w) { x.qU0[w] = p.hU0[w]; x.qRbw[w] = p.hRbw[w]; }
+            if (fmt == 0) {  // raw rows of the input for the general path (per-lane checks)
+                x.fastLo = src.in ? src.in_base : 0;
+                x.fastHi = src.in ? std::min(src.in_base + src.in_len, src.valid_end) : 0;
+            }
+        }
+    }
+    // small launches stage only the window [0, Wg) of one period: no ring wrap, no mirror rows
+    if (small && !x.bigSmall) {
+        Rt = R = (Wg + 15) / 16 * 16;
+        x.R = R; x.Rt = Rt; x.mirror = 0;
+    }
+    if (trace && x.qGroups > 0) fprintf(stderr, "hxq: qRbs=%d qGroups=%d workgroups=%lld\n", x.qRbs, x.qGroups, (long long)x.nblocks * x.qGroups);
     const size_t lds = hxsLds(Rt);
     const int64_t blocks = x.nblocks;
     if (hxt) {

@@ -105,6 +105,9 @@ struct HxsArgs {
     // p % stride == phase (phase = (role[w] >> 8) & 0xff, stride = role[w] >> 16)
     int ncomp;
     int role[12];
+    // hxq_kernel (small f32 STEREO / ROW16 launches): workgroup = (block, qRbs row blocks), qGroups per block
+    int qRbs, qGroups;
+    int qU0[12], qRbw[12];  // first window row / row block of each row-block program (HxDev::hU0)
 };
 typedef const __attribute__((address_space(4))) HxsArgs* HxsArgsP;
 
@@ -904,6 +907,49 @@ __global__ __launch_bounds__(64 * kHxsWaves) void hxs_kernel(HxsArgs x) {
                                           static_cast<int64_t>(gridDim.x) * blockDim.x);
 }
 
+// One compute wave of a small launch (one macro period per column): NS steps of 3 MFMAs over the
+// window image from LDS address aH (hi plane; lo plane at + dL), scale, store row block rbw of
+// block b's 16 columns.  Shared by hxs_small_kernel and hxq_kernel: identical bits.
+template <int NS, int VST>
+__device__ __forceinline__ void hxsSmallOut(const HxsArgs& x, uint32_t aH, uint32_t dL, const h8v* Ah, const h8v* Al, int b,
+                                            int rbw, int lane, int sh) {
+    const int grp = lane >> 4, l16 = lane & 15;
+    f32x4 nA = {0, 0, 0, 0}, nL = nA;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const h8v bh = bFragA(aH + 256 * s), bl = bFragA(aH + dL + 256 * s);
+        nA = mfma16(Ah[s], bh, nA);
+        nA = mfma16(Al[s], bh, nA);
+        nL = mfma16(Ah[s], bl, nL);
+    }
+    const f32x4 y = hxScale(nA, nL, sh);
+    const int col = b * 16 + l16;
+    const bool colOk = col < x.ncols;
+    const int kcol = col / x.C, ccol = col - kcol * x.C;
+    const int64_t a = x.a_lo + static_cast<int64_t>(kcol) * x.Np;  // Np == 1: the column's one period
+    const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;
+    const int64_t o0 = a * x.Pc + oRow0;
+    const bool fullRb = (rbw + 1) * 16 <= x.Pc;
+    const bool live = colOk && a < x.a_hi;
+    // whole-period stores need both lanes of a stereo pair (same chunk: same condition)
+    if (fullRb && live && (!x.out_pcm || VST == 4) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
+        char* pp = x.out + (o0 + (((VST == 2 || VST == 4) && (lane & 1)) ? 2 : 0)) * x.out_fs +
+                   ((VST == 2 || VST == 4) ? 0 : ccol * x.out_cs);
+        hxsStoreFast<VST>(x, pp, y, lane);
+    } else if (live) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t o = o0 + i;
+            if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi) {
+                char* pp = x.out + o * x.out_fs + ccol * x.out_cs;
+                if (x.out_pcm) pcmWrite(pp, 0, x.out_pcm, static_cast<double>(y[i]));
+                else if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
+                else *reinterpret_cast<float*>(pp) = y[i];
+            }
+        }
+    }
+}
+
 // Launch (explicitly instantiated in gar_hxs_i*.hip).
 // Small launches (x.small: stream chunks, flush tails -- one macro period per column): a compact
 // kernel of compute waves only, so the launch runs a short, warm instruction stream instead of the
@@ -962,43 +1008,9 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
         if (!hxsSmallFast(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag))
             hxsSmallStage(&x, b, static_cast<int>(threadIdx.x), static_cast<int>(blockDim.x), ring, QS, loudLo, loudHi, flag);
         __syncthreads();  // the whole window in the image
-        if (comp) {
-            const uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) + 8u * static_cast<uint32_t>(u0);
-            f32x4 nA = {0, 0, 0, 0}, nL = nA;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                const h8v bh = bFragA(aH + 256 * s), bl = bFragA(aH + dL + 256 * s);
-                nA = mfma16(Ah[s], bh, nA);
-                nA = mfma16(Al[s], bh, nA);
-                nL = mfma16(Ah[s], bl, nL);
-            }
-            const f32x4 y = hxScale(nA, nL, sh);
-            const int col = b * 16 + l16;
-            const bool colOk = col < x.ncols;
-            const int kcol = col / x.C, ccol = col - kcol * x.C;
-            const int64_t a = x.a_lo + static_cast<int64_t>(kcol) * x.Np;  // Np == 1: the column's one period
-            const int64_t oRow0 = static_cast<int64_t>(rbw) * 16 + 4 * grp;
-            const int64_t o0 = a * x.Pc + oRow0;
-            const bool fullRb = (rbw + 1) * 16 <= x.Pc;
-            const bool live = colOk && a < x.a_hi;
-            // whole-period stores need both lanes of a stereo pair (same chunk: same condition)
-            if (fullRb && live && (!x.out_pcm || VST == 4) && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
-                char* pp = x.out + (o0 + (((VST == 2 || VST == 4) && (lane & 1)) ? 2 : 0)) * x.out_fs +
-                           ((VST == 2 || VST == 4) ? 0 : ccol * x.out_cs);
-                hxsStoreFast<VST>(x, pp, y, lane);
-            } else if (live) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int64_t o = o0 + i;
-                    if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi) {
-                        char* pp = x.out + o * x.out_fs + ccol * x.out_cs;
-                        if (x.out_pcm) pcmWrite(pp, 0, x.out_pcm, static_cast<double>(y[i]));
-                        else if (x.out_f64) *reinterpret_cast<double*>(pp) = static_cast<double>(y[i]);
-                        else *reinterpret_cast<float*>(pp) = y[i];
-                    }
-                }
-            }
-        }
+        if (comp)
+            hxsSmallOut<NS, VST>(x, static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) + 8u * static_cast<uint32_t>(u0),
+                                 dL, Ah, Al, b, rbw, lane, sh);
         if (*flag) {  // uniform (LDS after the barrier)
             __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
@@ -1014,8 +1026,323 @@ __global__ __launch_bounds__(64 * kHxRbMaxWaves) void hxs_small_kernel(HxsArgs x
     }
 }
 
+// ---- hxq_kernel: small launches of f32 STEREO / ROW16 input over many workgroups ----------------
+// A 4096-frame stereo call is 28 macro periods x 2 channels = 56 columns = 4 blocks: on
+// hxs_small_kernel that is 4 workgroups, each gathering its whole window and running all row
+// blocks.  Here workgroup (b, g) runs row blocks [g*qRbs, (g+1)*qRbs) of block b (qRbs = 1: 40
+// workgroups for the stereo call): its waves load only the union of those row blocks' windows,
+// every row -- history seam and flush tail included -- through buffer loads (input and history
+// resources, per-lane selection, zeros past both), split it into the same f16 image and run the
+// same MFMA order and epilogue (hxsSmallOut): identical bits to hxs_small_kernel / hxs_kernel.
+constexpr int kHxqMaxWaves = 12;
+constexpr int kHxqB = 6;  // items per wave in flight (4 waves: 24 items, a 5-6 piece window in one round trip)
+
+struct HxqSrc {
+    __amdgpu_buffer_rsrc_t in, hist;
+    int64_t Tb;           // absolute row of the block's first chunk, row 0
+    int64_t fastLo, fastHi, hb, hlen, vend;
+    int rowB, hld;        // input row bytes, history row stride (elements)
+    bool useH;            // the block's window reaches into the history
+};
+
+// Sources of absolute row T: the input (inI: row T - Tb of the input resource) or the history (inH:
+// byte offset oh of element cH of its row); neither -> zeros.  Offsets past every record: 0x80000000.
+constexpr int kHxqOob = static_cast<int>(0x80000000u);
+__device__ __forceinline__ void hxqRow(const HxqSrc& q, int64_t T, int cH, bool& inI, bool& inH, int& oh) {
+    const int64_t h = T - q.hb;
+    inH = q.useH && T >= 0 && T < q.vend && h >= 0 && h < q.hlen;
+    inI = !inH && T >= q.fastLo && T < q.fastHi;
+    oh = inH ? (static_cast<int>(h) * q.hld + cH) * 4 : kHxqOob;
+}
+
+// Conversion of one item: row `row` of the image (column-relative row lo + row), quad q.
+__device__ __forceinline__ void hxqPut(char* ring, uint32_t QS, uint32_t Rt, int q, int row, int t, f32x4 e, int* loudLo,
+                                       int* loudHi, int* flag) {
+    const bool l0 = hxLoud(e[0]), l1 = hxLoud(e[1]), l2 = hxLoud(e[2]), l3 = hxLoud(e[3]);
+    if (__builtin_expect(l0 | l1 | l2 | l3, 0)) {
+        if (l0) { atomicMin(loudLo + 4 * q, t); atomicMax(loudHi + 4 * q, t); e[0] = 0.f; }
+        if (l1) { atomicMin(loudLo + 4 * q + 1, t); atomicMax(loudHi + 4 * q + 1, t); e[1] = 0.f; }
+        if (l2) { atomicMin(loudLo + 4 * q + 2, t); atomicMax(loudHi + 4 * q + 2, t); e[2] = 0.f; }
+        if (l3) { atomicMin(loudLo + 4 * q + 3, t); atomicMax(loudHi + 4 * q + 3, t); e[3] = 0.f; }
+        *flag = 1;
+    }
+    uint2 hv, lv;
+    hxSplit2(e[0], e[1], hv.x, lv.x);
+    hxSplit2(e[2], e[3], hv.y, lv.y);
+    char* qb = ring + q * QS + 8 * row;
+    *reinterpret_cast<uint2*>(qb) = hv;
+    *reinterpret_cast<uint2*>(qb + 8 * Rt) = lv;
+}
+
+// hxsFixup restricted to output rows [r0, r1) of each period (the workgroup's row blocks: another
+// workgroup owns -- and stores -- the other rows).
+__device__ __forceinline__ void hxqFixup(HxsArgsP xp, int b, const int* loudLo, const int* loudHi, int r0, int r1) {
+    const SrcDesc src = kload(&xp->src);
+    const OutDesc od = kload(&xp->od);
+    const int Qc = xp->Qc, Np = xp->Np, C = xp->C, ncols = xp->ncols, Pc = xp->Pc;
+    r1 = min(r1, Pc);
+    const int nr = r1 - r0;
+    const int64_t a_lo = xp->a_lo, a_hi = xp->a_hi;
+    for (int j = 0; j < 16; ++j) {
+        const int lo = loudLo[j], hi = loudHi[j];
+        const int col = b * 16 + j;
+        if (hi < 0 || col >= ncols || nr <= 0) continue;
+        const int k = col / C, c = col - k * C;
+        const int p0 = max(0, (lo - xp->Kread) / Qc), p1 = min(Np - 1, hi / Qc);
+        const int n = (p1 - p0 + 1) * nr;
+        for (int idx = threadIdx.x; idx < n; idx += blockDim.x) {
+            const int p = p0 + idx / nr, r = r0 + (idx - (idx / nr) * nr);
+            const int64_t a = a_lo + static_cast<int64_t>(k) * Np + p;
+            if (a >= a_hi) continue;
+            const int64_t o = a * Pc + r;
+            if (o < od.o_lo || o >= od.o_hi) continue;
+            const int w0 = p * Qc + xp->rowOff[r], w1 = w0 + xp->rowLen[r];
+            if (w1 <= lo || w0 > hi) continue;
+            const int64_t t0 = a * Qc + xp->rowOff[r];
+            bool loud = false;
+            for (int kk = 0; kk < w1 - w0 && !loud; ++kk) loud = hxLoud(srcRead<float>(src, t0 + kk, c));
+            if (loud) outWrite<float>(od, o, c, static_cast<float>(hxsExact(xp, a, r, c)));
+        }
+    }
+}
+
+template <int NS, int VST>
+__global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t Rt = static_cast<uint32_t>(x.Rt), QS = 16u * Rt + 64u;
+    char* ring = reinterpret_cast<char*>(smem);
+    int* loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(QS));
+    int* loudHi = loudLo + 16;
+    int* flag = loudHi + 16;
+    const int lane = threadIdx.x & 63;
+    const int w = uni(threadIdx.x >> 6), nw = uni(blockDim.x >> 6);
+    const unsigned long long tEntry = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rEntry = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int b = uni(blockIdx.x / x.qGroups);
+    const int r0 = uni((blockIdx.x - b * x.qGroups) * x.qRbs);
+    const int nrw = min(x.qRbs, x.nprog - r0);
+    // union window [lo, lo + nrow) of the workgroup's row blocks (column-relative rows)
+    int lo = INT_MAX, hi = 0;
+    for (int i = 0; i < nrw; ++i) {
+        const int u = x.qU0[r0 + i];
+        lo = min(lo, u);
+        hi = max(hi, u);
+    }
+    const int nrow = hi + 32 * NS - lo;
+    const bool comp = w < nrw;
+    h8v Ah[NS], Al[NS];
+    int u0 = 0, rbw = 0;
+    if (comp) {  // A lands while the window loads
+        const int wt = r0 + w;
+        u0 = x.qU0[wt];
+        rbw = x.qRbw[wt];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            Ah[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 0) * 64 + lane];
+            Al[s] = x.A[((static_cast<size_t>(wt) * NS + s) * 2 + 1) * 64 + lane];
+        }
+    }
+    const HxsArgsP xc = hxsCold();
+    const SrcDesc src = kload(&xc->src);
+    // load sources
+    HxqSrc q;
+    const int col0 = b * 16, kb = col0 / x.C, c0 = col0 - kb * x.C;
+    const int chunkRows = x.Np * x.Qc;
+    q.Tb = hxsChunkRow(&x, kb, 0);
+    q.fastLo = x.fastLo;
+    q.fastHi = x.fastHi;
+    q.hb = src.hist_base;
+    q.hlen = src.hist ? src.hist_len : 0;
+    q.vend = src.valid_end;
+    q.rowB = static_cast<int>(x.in_fs) * 4;
+    q.hld = static_cast<int>(src.hist_ld);
+    if (x.fmt == 0)  // per-lane checks guard every load (host: every offset < 2^31)
+        q.in = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(x.in + q.Tb * x.in_fs * x.in_esz), 0, 0x7fffffff, 0x00020000);
+    else
+        q.in = hxsRsrcT(&x, q.Tb, x.fmt == 2 ? c0 : 0, x.fmt == 2 ? 64 : 8);
+    {
+        const int64_t hrows = min(q.hlen, q.vend - q.hb);
+        const int64_t nb = hrows > 0 ? hrows * q.hld * 4 : 0;
+        q.hist = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(src.hist), 0, static_cast<int>(nb < 0x7fffffff ? nb : 0x7fffffff),
+                                                   0x00020000);
+    }
+    q.useH = q.hlen > 0 && q.Tb + lo < q.hb + q.hlen;  // uniform: some row of the block's window is history
+    // history keep for the next call (rows [ht0, ht0 + hn) of the stream): the first kHk elements of
+    // this thread up front, through buffer loads (vector-memory counter only: a flat load would also
+    // hold every LDS wait and barrier of the window staging until it lands)
+    constexpr int kHk = 2;
+    const int64_t hme = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t hnth = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t htot = x.hn * x.C;
+    float hk[kHk];
+    if (x.hn > 0) {
+        HxqSrc qk = q;
+        qk.useH = q.hlen > 0;
+        const __amdgpu_buffer_rsrc_t rk =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(x.in + x.ht0 * x.in_fs * x.in_esz), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < kHk; ++u) {
+            const int64_t i = hme + u * hnth;
+            const int64_t t = i / x.C;
+            const int c = static_cast<int>(i - t * x.C);
+            bool inI, inH;
+            int oh;
+            hxqRow(qk, i < htot ? x.ht0 + t : -1, c, inI, inH, oh);
+            const int oi = inI ? static_cast<int>((t * x.in_fs + static_cast<int64_t>(c) * x.in_cs) * x.in_esz) : kHxqOob;
+            const float vi = x.in_esz == 8 ? static_cast<float>(__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rk, oi, 0, 0)))
+                                           : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rk, oi, 0, 0));
+            const float vh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(qk.hist, oh, 0, 0));
+            hk[u] = inH ? vh : vi;
+        }
+    }
+    // loud state reset, then a barrier before any conversion: placed after the first batch's loads
+    // issue (every wave runs one batch at least), so the barrier overlaps their round trip
+    auto loudReset = [&]() {
+        if (threadIdx.x < 16) { loudLo[threadIdx.x] = INT_MAX; loudHi[threadIdx.x] = -1; }
+        if (threadIdx.x == 0) *flag = 0;
+        hxsBarrier();
+    };
+    unsigned long long tB1 = 0;
+    if (x.fmt == 1) {  // STEREO: item = (quad, 64-row piece), chunks 2q, 2q+1 of the block (both channels)
+        const int nit = 4 * ((nrow + 63) >> 6);
+        for (int it0 = w, first = 1; first || it0 < nit; it0 += kHxqB * nw) {
+            f2v a[kHxqB], c[kHxqB], ah[kHxqB], ch[kHxqB];
+            bool hA[kHxqB], hC[kHxqB];
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw, qd = it & 3, pc = it >> 2;
+                const int t = lo + 64 * pc + lane;
+                const bool on = it < nit && 64 * pc + lane < nrow;
+                const int64_t T0 = q.Tb + static_cast<int64_t>(2 * qd) * chunkRows + t;
+                int oh0, oh1;
+                bool i0, i1;
+                hxqRow(q, on ? T0 : -1, 0, i0, hA[u], oh0);
+                hxqRow(q, on ? T0 + chunkRows : -1, 0, i1, hC[u], oh1);
+                const int oi0 = i0 ? static_cast<int>(T0 - q.Tb) * q.rowB : kHxqOob;
+                const int oi1 = i1 ? static_cast<int>(T0 + chunkRows - q.Tb) * q.rowB : kHxqOob;
+                a[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(q.in, oi0, 0, 0));
+                c[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(q.in, oi1, 0, 0));
+                if (q.useH) {
+                    ah[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(q.hist, oh0, 0, 0));
+                    ch[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(q.hist, oh1, 0, 0));
+                }
+            }
+            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw, pc = it >> 2, row = 64 * pc + lane;
+                if (it < nit && row < nrow) {
+                    const f2v va = (q.useH && hA[u]) ? ah[u] : a[u];
+                    const f2v vc = (q.useH && hC[u]) ? ch[u] : c[u];
+                    hxqPut(ring, QS, Rt, it & 3, row, lo + row, f32x4{va.x, va.y, vc.x, vc.y}, loudLo, loudHi, flag);
+                }
+            }
+        }
+    } else if (x.fmt == 0) {  // any other f32 / f64 layout: item = (quad, 64-row piece), one element load per column
+        const int nit = 4 * ((nrow + 63) >> 6);
+        const int esz = x.in_esz;
+        for (int it0 = w, first = 1; first || it0 < nit; it0 += kHxqB * nw) {
+            f32x4 v[kHxqB], vh[kHxqB];
+            bool hV[kHxqB][4];
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw, qd = it & 3, pc = it >> 2;
+                const int row = 64 * pc + lane;
+                const bool on = it < nit && row < nrow;
+#pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const int col = col0 + 4 * qd + n, k = col / x.C, c = col - k * x.C;  // wave-uniform
+                    const int64_t dT = static_cast<int64_t>(k - kb) * chunkRows + lo + row;  // T - Tb
+                    int oh;
+                    bool inI;
+                    hxqRow(q, on ? q.Tb + dT : -1, c, inI, hV[u][n], oh);
+                    const int oi = inI ? static_cast<int>((dT * x.in_fs + static_cast<int64_t>(c) * x.in_cs) * esz) : kHxqOob;
+                    if (esz == 8) v[u][n] = static_cast<float>(__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(q.in, oi, 0, 0)));
+                    else v[u][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(q.in, oi, 0, 0));
+                    if (q.useH) vh[u][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(q.hist, oh, 0, 0));
+                }
+            }
+            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw, row = 64 * (it >> 2) + lane;
+                if (it < nit && row < nrow) {
+                    f32x4 e = v[u];
+                    if (q.useH) {
+#pragma unroll
+                        for (int n = 0; n < 4; ++n) e[n] = hV[u][n] ? vh[u][n] : e[n];
+                    }
+                    hxqPut(ring, QS, Rt, it & 3, row, lo + row, e, loudLo, loudHi, flag);
+                }
+            }
+        }
+    } else {  // ROW16: item = 16-row piece, lane = 16 quad + row: channels c0 + 4 quad .. + 3 of chunk kb
+        const int nit = (nrow + 15) >> 4;
+        const int qd = lane >> 4;
+        for (int it0 = w, first = 1; first || it0 < nit; it0 += kHxqB * nw) {
+            f32x4 v[kHxqB], vh[kHxqB];
+            bool hV[kHxqB];
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw;
+                const int row = 16 * it + (lane & 15);
+                const bool on = it < nit && row < nrow;
+                int oh;
+                bool inI;
+                hxqRow(q, on ? q.Tb + lo + row : -1, c0 + 4 * qd, inI, hV[u], oh);
+                const int oi = inI ? (lo + row) * q.rowB + 16 * qd : kHxqOob;
+                v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(q.in, oi, 0, 0));
+                if (q.useH) vh[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(q.hist, oh, 0, 0));
+            }
+            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+#pragma unroll
+            for (int u = 0; u < kHxqB; ++u) {
+                const int it = it0 + u * nw, row = 16 * it + (lane & 15);
+                if (it < nit && row < nrow) hxqPut(ring, QS, Rt, qd, row, lo + row, (q.useH && hV[u]) ? vh[u] : v[u], loudLo, loudHi, flag);
+            }
+        }
+    }
+    hxsBarrier();  // the window image complete
+    const unsigned long long tImg = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+    if (comp) {
+        const int grp = lane >> 4, l16 = lane & 15;
+        const uint32_t laneOff = (l16 & 3) * QS + 8u * (4 * grp + (l16 >> 2));
+        hxsSmallOut<NS, VST>(x, static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(ring + laneOff))) + 8u * static_cast<uint32_t>(u0 - lo),
+                             8u * Rt, Ah, Al, b, rbw, lane, -(x.ea + kHxXs));
+    }
+    if (*flag) {  // uniform (LDS after the barrier)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        hxqFixup(hxsCold(), b, loudLo, loudHi, 16 * r0, 16 * (r0 + nrw));
+    }
+    const unsigned long long tOut = (kHxsDev && x.prof) ? __builtin_amdgcn_s_memtime() : 0;
+    if (x.hn > 0) {
+#pragma unroll
+        for (int u = 0; u < kHk; ++u)
+            if (hme + u * hnth < htot) x.hdst[hme + u * hnth] = hk[u];
+        if (htot > kHk * hnth) hxsHistKeep(x, hme + kHk * hnth, hnth);
+    }
+    if (kHxsDev && x.prof && threadIdx.x == 0) {  // development: wave 0's phases, workgroup life, launch span
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tEnd = __builtin_amdgcn_s_memtime(), rEnd = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(x.prof + 40, tB1 - tEntry);
+        atomicAdd(x.prof + 41, tImg - tB1);
+        atomicAdd(x.prof + 42, tOut - tImg);
+        atomicAdd(x.prof + 43, tEnd - tOut);
+        atomicAdd(x.prof + 44, 1ull);
+        atomicMin(x.prof + 10, rEntry);
+        atomicMax(x.prof + 11, rEnd);
+        if (blockIdx.x < 4096) { x.prof[64 + 2 * blockIdx.x] = rEntry; x.prof[65 + 2 * blockIdx.x] = rEnd - rEntry; }
+    }
+}
+
 template <int NS, int VST>
 hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
+    if (x.small && x.qGroups > 0) {  // hxq_kernel: (block, row-block group) workgroups
+        if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxq_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
+        hipLaunchKernelGGL((hxq_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks * x.qGroups)), dim3(64 * max(4, x.qRbs)), lds, st, x);
+        return hipGetLastError();
+    }
     if (x.small && !x.bigSmall) {
         if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
         hipLaunchKernelGGL((hxs_small_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * x.nprog), lds, st, x);

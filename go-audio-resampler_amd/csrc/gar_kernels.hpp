@@ -88,6 +88,7 @@ struct HxDev {
     int* fix;            // [1 + fixCap]: interior blocks holding loud elements (count first)
     int fixCap;
     int hxsOk;           // host: the plan fits hxs_kernel (hxsPlanFits), so fused PCM I/O can use it
+    int hU0[16], hRbw[16];  // host copies of each row-block program's first row / row block (rb mode, nw <= 16)
 };
 
 // General polyphase stage with live cubic coefficient interpolation

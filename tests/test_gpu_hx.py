@@ -176,3 +176,25 @@ def test_hx_loud_many_columns(gar, O, cuda):
         big = np.abs(np.asarray(want[c])) > 20
         assert big.any()
         assert np.max(np.abs(got[big, c] - want[c][big]) / np.abs(want[c][big])) <= 1e-6
+
+
+@pytest.mark.parametrize("chunk", [4096, 1500])
+def test_hx_row16_small_launches_loud(gar, O, cuda, chunk):
+    """16 channels fed in short calls: every launch is a small ROW16 launch (hxq_kernel: one
+    workgroup per block and row-block group, history seam loaded through the history resource),
+    with loud samples in many columns -- the same bits as the one-shot call, exact where loud."""
+    n, ch = 40000, 16
+    x = signal(n, ch, 48000, seed=23).astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(9)
+    for c in range(ch):
+        for t in rng.integers(0, n, size=3):
+            x[t, c] = (1 if rng.random() < 0.5 else -1) * 10.0 ** rng.uniform(1.3, 4)
+    x = x.astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 48000, 44100, x, gar.QualityVeryHigh, gar.F32, chunk_sizes(n, chunk))
+    one = run(gar, cuda, 48000, 44100, x, gar.QualityVeryHigh, gar.F32)
+    np.testing.assert_array_equal(got, one)
+    want = oracle_new(O, 48000, 44100, x, O.P_VERYHIGH)
+    for c in range(ch):
+        big = np.abs(np.asarray(want[c])) > 20
+        assert big.any()
+        assert np.max(np.abs(got[big, c] - want[c][big]) / np.abs(want[c][big])) <= 1e-6
