@@ -800,10 +800,10 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
         if constexpr (sizeof(TC) == 8 && NS <= kBgRbMaxSteps) {
             if (threads > 64 * kBgRbMaxWaves) return hipErrorInvalidConfiguration;
             if (g.rbMode == 2) {  // time-major, LDS-staged windows
-                if (setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)) < lds) return hipErrorOutOfMemory;
+                if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)); lim_ < lds) return ldsTooBig("bg_rt_kernel", lds, lim_);
                 hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
             } else if (g.rbMode == 3) {  // column blocks, row-major LDS-staged windows
-                if (setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rc_kernel<TC, NS>)) < lds) return hipErrorOutOfMemory;
+                if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rc_kernel<TC, NS>)); lim_ < lds) return ldsTooBig("bg_rc_kernel", lds, lim_);
                 hipLaunchKernelGGL((bg_rc_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
             } else {
                 hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);

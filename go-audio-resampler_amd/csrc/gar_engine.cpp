@@ -1175,11 +1175,20 @@ struct DeviceGuard {
     DeviceGuard& operator=(const DeviceGuard&) = delete;
 };
 
+thread_local bool g_launchLimit = false;  // the last wrap() failed on a launch limit (callOn poisons the handle)
+
 template <class F>
 gar_status wrap(F&& f) {
+    g_launchLimit = false;
     try {
         return f();
     } catch (const DevError& e) {
+        if (e.e == hipErrorInvalidConfiguration && !launchLimitMsg().empty()) {  // a launch the device cannot run
+            g_err = launchLimitMsg() + " (at " + e.what + ")";
+            launchLimitMsg().clear();
+            g_launchLimit = true;
+            return GAR_ERR_INVALID_ARGUMENT;
+        }
         g_err = std::string("HIP error ") + hipGetErrorString(e.e) + " at " + e.what;
         return GAR_ERR_DEVICE;
     } catch (const std::bad_alloc&) {
@@ -1208,7 +1217,7 @@ gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
         }
         return r;
     });
-    if (st == GAR_ERR_DEVICE) {
+    if (st == GAR_ERR_DEVICE || (st == GAR_ERR_INVALID_ARGUMENT && g_launchLimit)) {  // state may be half-updated
         h->poisoned = true;
         h->failStream = s;
     }

@@ -339,6 +339,10 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
             for (int cand = p.nw; cand >= 1; --cand)
                 if (x.nblocks * static_cast<int64_t>(cdiv(p.nw, cand)) >= static_cast<int64_t>(ncu)) { nr = cand; break; }
             if (knobHxqNr > 0) nr = std::min(knobHxqNr, p.nw);
+            // variant 1 (same-run A/B, profiles/r04j_hxq_variants.txt): the first barrier after the first load
+            // batch issues, history keep by gathers -- workgroup life 6.0 us; buffer-load history keep 6.6 us
+            static const int knobOpt = std::getenv("GAR_HXQ_OPT") ? std::atoi(std::getenv("GAR_HXQ_OPT")) : 1;
+            x.qOpt = knobOpt;
             x.qRbs = nr;
             x.qGroups = static_cast<int>(cdiv(p.nw, nr));
             for (int w = 0; w < p.nw; ++w) { x.qU0[w] = p.hU0[w]; x.qRbw[w] = p.hRbw[w]; }

@@ -108,6 +108,7 @@ struct HxsArgs {
     // hxq_kernel (small f32 STEREO / ROW16 launches): workgroup = (block, qRbs row blocks), qGroups per block
     int qRbs, qGroups;
     int qU0[12], qRbw[12];  // first window row / row block of each row-block program (HxDev::hU0)
+    int qOpt;               // hxq_kernel variants (GAR_HXQ_OPT): 1 barrier after the first load batch issues, 2 buffer-load history keep
 };
 typedef const __attribute__((address_space(4))) HxsArgs* HxsArgsP;
 
@@ -1175,7 +1176,15 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
     const int64_t hnth = static_cast<int64_t>(gridDim.x) * blockDim.x;
     const int64_t htot = x.hn * x.C;
     float hk[kHk];
-    if (x.hn > 0) {
+    if (x.hn > 0 && !(x.qOpt & 2)) {  // variant: flat gathers
+#pragma unroll
+        for (int u = 0; u < kHk; ++u) {
+            const int64_t i = hme + u * hnth;
+            const int64_t t = i / x.C;
+            hk[u] = i < htot ? hxsGather(src, x.ht0 + t, static_cast<int>(i - t * x.C), x.A) : 0.f;
+        }
+    }
+    if (x.hn > 0 && (x.qOpt & 2)) {
         HxqSrc qk = q;
         qk.useH = q.hlen > 0;
         const __amdgpu_buffer_rsrc_t rk =
@@ -1203,6 +1212,8 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
         hxsBarrier();
     };
     unsigned long long tB1 = 0;
+    const bool early = x.qOpt & 1;
+    if (!early) { loudReset(); if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
     if (x.fmt == 1) {  // STEREO: item = (quad, 64-row piece), chunks 2q, 2q+1 of the block (both channels)
         const int nit = 4 * ((nrow + 63) >> 6);
         for (int it0 = w, first = 1; first || it0 < nit; it0 += kHxqB * nw) {
@@ -1227,7 +1238,8 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
                     ch[u] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(q.hist, oh1, 0, 0));
                 }
             }
-            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            if (first && early) { loudReset(); if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            first = 0;
 #pragma unroll
             for (int u = 0; u < kHxqB; ++u) {
                 const int it = it0 + u * nw, pc = it >> 2, row = 64 * pc + lane;
@@ -1262,7 +1274,8 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
                     if (q.useH) vh[u][n] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(q.hist, oh, 0, 0));
                 }
             }
-            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            if (first && early) { loudReset(); if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            first = 0;
 #pragma unroll
             for (int u = 0; u < kHxqB; ++u) {
                 const int it = it0 + u * nw, row = 64 * (it >> 2) + lane;
@@ -1294,7 +1307,8 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
                 v[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(q.in, oi, 0, 0));
                 if (q.useH) vh[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(q.hist, oh, 0, 0));
             }
-            if (first) { loudReset(); first = 0; if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            if (first && early) { loudReset(); if (kHxsDev && x.prof) tB1 = __builtin_amdgcn_s_memtime(); }
+            first = 0;
 #pragma unroll
             for (int u = 0; u < kHxqB; ++u) {
                 const int it = it0 + u * nw, row = 16 * it + (lane & 15);
@@ -1339,16 +1353,18 @@ __global__ __launch_bounds__(64 * kHxqMaxWaves) void hxq_kernel(HxsArgs x) {
 template <int NS, int VST>
 hipError_t hxsLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
     if (x.small && x.qGroups > 0) {  // hxq_kernel: (block, row-block group) workgroups
-        if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxq_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
-        hipLaunchKernelGGL((hxq_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks * x.qGroups)), dim3(64 * max(4, x.qRbs)), lds, st, x);
+        if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&hxq_kernel<NS, VST>)); lim_ < lds) return ldsTooBig("hxq_kernel", lds, lim_);
+        static const int knobW = std::getenv("GAR_HXQ_W") ? std::atoi(std::getenv("GAR_HXQ_W")) : 4;  // waves per workgroup (>= qRbs)
+        const int nw = std::min(kHxqMaxWaves, std::max(std::max(knobW, 1), x.qRbs));
+        hipLaunchKernelGGL((hxq_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks * x.qGroups)), dim3(64 * nw), lds, st, x);
         return hipGetLastError();
     }
     if (x.small && !x.bigSmall) {
-        if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
+        if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_small_kernel<NS, VST>)); lim_ < lds) return ldsTooBig("hxs_small_kernel", lds, lim_);
         hipLaunchKernelGGL((hxs_small_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * x.nprog), lds, st, x);
         return hipGetLastError();
     }
-    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>)) < lds) return hipErrorOutOfMemory;
+    if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&hxs_kernel<NS, VST>)); lim_ < lds) return ldsTooBig("hxs_kernel", lds, lim_);
     hipLaunchKernelGGL((hxs_kernel<NS, VST>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.nprog + kHxsLoaders)), lds, st, x);
     return hipGetLastError();
 }

@@ -485,7 +485,7 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
 template <int NS, int FMT, int VST, int NL>
 hipError_t hxtLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) {
     if (x.ncomp + NL > kHxtWaves) return hipErrorInvalidConfiguration;
-    if (setMaxLdsOnce(reinterpret_cast<const void*>(&hxt_kernel<NS, FMT, VST, NL>)) < lds) return hipErrorOutOfMemory;
+    if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&hxt_kernel<NS, FMT, VST, NL>)); lim_ < lds) return ldsTooBig("hxt_kernel", lds, lim_);
     hipLaunchKernelGGL((hxt_kernel<NS, FMT, VST, NL>), dim3(static_cast<unsigned>(blocks)), dim3(64 * (x.ncomp + NL)), lds,
                        st, x);
     return hipGetLastError();

@@ -32,6 +32,16 @@ namespace gar {
 // Raises the kernel's dynamic-LDS limit to what the CU leaves next to its static LDS (160 KiB -
 // static; asking for 160 KiB with static LDS present fails, and a launch above the default limit
 // then fails with "invalid argument").  Returns the dynamic-LDS limit in force (bytes).
+std::string& launchLimitMsg() {
+    static thread_local std::string m;
+    return m;
+}
+hipError_t ldsTooBig(const char* kernel, size_t need, size_t limit) {
+    launchLimitMsg() = std::string(kernel) + " needs " + std::to_string(need) + " B of dynamic LDS; the device allows " +
+                       std::to_string(limit) + " B for it";
+    return hipErrorInvalidConfiguration;
+}
+
 size_t setMaxLdsOnce(const void* fn) {
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, size_t> done;

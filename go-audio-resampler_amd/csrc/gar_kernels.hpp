@@ -1,5 +1,6 @@
 // gar_kernels.hpp -- device-side descriptors and launchers (gar_kernels.hip).
 #pragma once
+#include <string>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -50,6 +51,12 @@ __host__ __device__ inline void pcmWrite(void* p, int64_t e, int bits, double y)
 }
 
 struct HxDev;
+
+// A launch whose configuration the device cannot run (dynamic LDS above the kernel's limit): the
+// launcher records what was exceeded here and returns hipErrorInvalidConfiguration; the C-ABI turns
+// it into GAR_ERR_INVALID_ARGUMENT with this message (gar_engine.cpp wrap).
+std::string& launchLimitMsg();
+hipError_t ldsTooBig(const char* kernel, size_t need, size_t limit);
 
 // Device copy of a BgPlan (gar_plan.hpp).
 struct BgDev {
