@@ -873,6 +873,10 @@ __device__ __forceinline__ void hxsRegLoadersT(const HxsArgs& x, const HxsShared
 }
 
 __device__ __forceinline__ void hxsRegLoaders(const HxsArgs& x, const HxsShared& sh_, int l, int lane) {
+#ifdef GAR_HXS_ONLYFMT  // development: one loader format per build (register-allocation studies)
+    hxsRegLoadersT<GAR_HXS_ONLYFMT>(x, sh_, l, lane);
+    return;
+#endif
     if (x.fmt == 1) hxsRegLoadersT<1>(x, sh_, l, lane);
     else if (x.fmt == 2) hxsRegLoadersT<2>(x, sh_, l, lane);
     else if (x.fmt == 3) hxsRegLoadersT<3>(x, sh_, l, lane);

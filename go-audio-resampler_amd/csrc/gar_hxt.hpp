@@ -109,11 +109,18 @@ __device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT, NL>& r, int k) {
     else return r.v[k];
 }
 
-// Exact per-element path of a load that holds a loud element (rare, out of line): loader l's items
+// Exact per-element path of a load that holds a loud element (rare): loader l's items
 // of the load again, re-read from memory through the SrcDesc with the fast path's item mapping and
 // staged through hxsPutItem (loud elements as zero, their column rows recorded).
+// Inlined (default): as out-of-line calls, the calling convention's register saves made the
+// allocator spill a load's destination right after the issue, so every loader step waited for
+// its own loads (kHxtD-deep pipeline serialised; 61 us of cfg2's 163 us) -- GAR_HXT_SLOW_ATTR=__noinline__
+// restores the calls for A/B.
+#ifndef GAR_HXT_SLOW_ATTR
+#define GAR_HXT_SLOW_ATTR __forceinline__
+#endif
 template <int FMT, int NL>
-__device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
+__device__ GAR_HXT_SLOW_ATTR void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l, int lane, HxsShared sh) {
     const SrcDesc src = kload(&xp->src);
     const int p0 = uni(st.T0 % xp->R);
     for (int k = 0; k < hxtItems<NL>(); ++k) {
@@ -144,7 +151,7 @@ __device__ __noinline__ void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, int l,
 // Edge load (rows before the raw input, partial blocks, any other layout): every element gathered
 // through the SrcDesc (history | input | zeros); out of line.  Loader l takes items l, l+4, ...
 // of the 4 quads x ceil(nrow/64) pieces.
-__device__ __noinline__ void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int nl, int lane, HxsShared sh) {
+__device__ GAR_HXT_SLOW_ATTR void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int nl, int lane, HxsShared sh) {
     const SrcDesc src = kload(&xp->src);
     const int p0 = uni(st.T0 % xp->R);
     const int nit = 4 * ((st.nrow + 63) >> 6);
@@ -297,7 +304,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (j >= P) {
                     if (j == P) p0 = Wg;  // Wg < R
                     need = last < 0 ? 0 : need + 1;
-                    if (need > 0) hxtWait(sy.cp, x.ncomp, need);
+                    if (need > 0 && !(dbg & 64)) hxtWait(sy.cp, x.ncomp, need);  // development 64: loaders never wait
                     last += GQ;
                 }
                 if (!((dbg & 16) && j >= P)) {
@@ -357,7 +364,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         while (first < p0) first += ro.st;
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
-            hxtWait(sy.ld, kHxtLdSlots, P + g);  // loads 0 .. P+g-1: stage 0 and stages 1 .. g in the ring
+            if (!(dbg & 32)) hxtWait(sy.ld, kHxtLdSlots, P + g);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
             // the lane's ring offset, recomputed per group (a value held across the group loop spills,
             // and its reload's vmcnt(0) would wait for this wave's output stores)
             int ln = lane;
@@ -365,7 +372,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
             const uint32_t lo = ((ln & 15) & 3) * sh_.QS + 8u * (4 * (ln >> 4) + ((ln & 15) >> 2));
             uint32_t aH = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_s4p)(sh_.ring))) + lo + 8u * static_cast<uint32_t>(u0) +
                           8u * static_cast<uint32_t>((g % nslot) * GQ) + 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(first - p0);
-            h8v bh0 = bFragA(aH), bl0 = bFragA(aH + dL);
+            h8v bh0 = (dbg & 8) ? h8v{} : bFragA(aH), bl0 = (dbg & 8) ? h8v{} : bFragA(aH + dL);  // development 8: no B reads
             for (int i = 0; i < n; ++i) {
                 asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
                 const bool last = i + 1 == n;
@@ -375,7 +382,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
                 for (int s = 0; s < NS; ++s) {
                     const int ug = (s + 1) / NS, us = (s + 1) % NS;
                     h8v bhn = bh0, bln = bl0;
-                    if (!(ug == 1 && last)) {
+                    if (!(ug == 1 && last) && !(dbg & 8)) {
                         bhn = bFragA((ug == 0 ? aH : aN) + 256 * us);
                         bln = bFragA((ug == 0 ? aL : aNL) + 256 * us);
                     }
