@@ -400,23 +400,28 @@ template <int FMT>
 __device__ __forceinline__ bool hxsRegIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxsRegBuf<FMT>& r) {
     const bool fast = FMT != 0 && live && st.fast;
     const int npc = fast ? (st.nrow + 63) >> 6 : 0;
-    const int base = st.T0 * rs.rowB + rs.lane0;
+    // loader index and strides opaque per call: otherwise every item's offset and mask is hoisted out
+    // of the step loop into SGPRs, which spill (v_readlane per item and step)
+    int lq = l;
+    HxsRegSrc rq = rs;
+    asm volatile("" : "+s"(lq), "+s"(rq.rowB), "+s"(rq.chunkB));
+    const int base = st.T0 * rq.rowB + rq.lane0;
 #pragma unroll
     for (int k = 0; k < kHxsItems; ++k) {
-        const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
+        const int it = lq + k * kHxsLoaders, q = it & 3, i = it >> 2;
         const bool on = it < 4 * kHxsNP && i < npc;
         if constexpr (FMT == 2) {  // item = 16-row piece (all four quads)
             const bool on16 = it < 4 * kHxsNP && 16 * it < (fast ? st.nrow : 0);
-            const int o = on16 ? base + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
+            const int o = on16 ? base + 16 * it * rq.rowB : static_cast<int>(0x80000000u);
             r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
         } else if constexpr (FMT == 1 || FMT == 4) {  // f32 / int32 stereo frames
-            const int o = on ? base + 64 * i * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
-            const int o2 = on ? o + rs.chunkB : o;
+            const int o = on ? base + 64 * i * rq.rowB + 2 * q * rq.chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + rq.chunkB : o;
             r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
             r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
         } else if constexpr (FMT == 3) {  // int16 stereo frames
-            const int o = on ? base + 64 * i * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
-            const int o2 = on ? o + rs.chunkB : o;
+            const int o = on ? base + 64 * i * rq.rowB + 2 * q * rq.chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + rq.chunkB : o;
             r.a[k] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, o, 0, 0);
             r.b[k] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, o2, 0, 0);
         }
@@ -553,9 +558,11 @@ __device__ __forceinline__ void hxsRegConvert(XP x, const HxsStage& st, bool fas
                                               int b, int l, int lane, const HxsShared& sh) {
     const int p0 = uni(st.T0 % x->R);
     if (FMT != 0 && fast) {  // straight-line: registers -> ring
+        int lq = l;  // opaque per call (hxsRegIssue)
+        asm volatile("" : "+s"(lq));
 #pragma unroll
         for (int k = 0; k < kHxsItems; ++k) {
-            const int it = l + k * kHxsLoaders, q = it & 3, i = it >> 2;
+            const int it = lq + k * kHxsLoaders, q = it & 3, i = it >> 2;
             if constexpr (FMT == 2) {
                 const int row = 16 * it + (lane & 15);
                 if (it < 4 * kHxsNP && 16 * it < st.nrow && row < st.nrow)

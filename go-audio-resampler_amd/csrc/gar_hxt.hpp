@@ -68,20 +68,24 @@ template <int FMT, int NL>
 __device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const HxsRegSrc& rs, int l, HxtBuf<FMT, NL>& r) {
     const bool fast = live && st.fast;
     const int nrow = fast ? st.nrow : 0;
-    const int base = st.T0 * rs.rowB + rs.lane0;
+    // loader index and strides opaque per call: otherwise every item's offset and mask is hoisted out
+    // of the step loop into SGPRs, which spill (one v_readlane per item and step)
+    int lq = l, rowB = rs.rowB, chunkB = rs.chunkB;
+    asm volatile("" : "+s"(lq), "+s"(rowB), "+s"(chunkB));
+    const int base = st.T0 * rowB + rs.lane0;
 #pragma unroll
     for (int k = 0; k < hxtItems<NL>(); ++k) {
         if constexpr (FMT == 1) {  // item it: quad q = chunks 2q, 2q+1; piece it >> 2 = rows 64 (it >> 2) ..
-            const int it = l + NL * k, q = it & 3, pc = it >> 2;
+            const int it = lq + NL * k, q = it & 3, pc = it >> 2;
             const bool on = pc < hxtPieces(NL) && 64 * pc < nrow;
-            const int o = on ? base + 64 * pc * rs.rowB + 2 * q * rs.chunkB : static_cast<int>(0x80000000u);
-            const int o2 = on ? o + rs.chunkB : o;
+            const int o = on ? base + 64 * pc * rowB + 2 * q * chunkB : static_cast<int>(0x80000000u);
+            const int o2 = on ? o + chunkB : o;
             r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
             r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
         } else {  // 16-row piece l + NL k, lane = 16 quad + row
-            const int it = l + NL * k;
+            const int it = lq + NL * k;
             const bool on = 16 * it < nrow;
-            const int o = on ? base + 16 * it * rs.rowB : static_cast<int>(0x80000000u);
+            const int o = on ? base + 16 * it * rowB : static_cast<int>(0x80000000u);
             r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
         }
     }
@@ -178,20 +182,20 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
     const int nrow = st.nrow;
     // opaque per call: the compiler must not hoist the items' row numbers out of the step loop
     // (ten live row registers spill, and every reload's vmcnt(0) waits for the loads in flight)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
+    int ln = lane, lq = l;
+    asm volatile("" : "+v"(ln), "+s"(lq));
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < hxtItems<NL>(); ++k) {
         int row, q;
         bool on;
         if constexpr (FMT == 1) {
-            const int it = l + NL * k, pc = it >> 2;
+            const int it = lq + NL * k, pc = it >> 2;
             on = pc < hxtPieces(NL) && 64 * pc < nrow;
             row = 64 * pc + ln;
             q = it & 3;
         } else {
-            const int it = l + NL * k;
+            const int it = lq + NL * k;
             on = 16 * it < nrow;
             row = 16 * it + (ln & 15);
             q = ln >> 4;
