@@ -45,6 +45,9 @@ unsigned long long* profBuf() {
                                        static_cast<double>(h[20]) / h[23], static_cast<double>(h[21]) / h[23], static_cast<double>(h[22]) / h[23], h[23]);
                     if (h[23]) fprintf(stderr, "hxs wave-0: entry->A landed %.0f, entry->barrier 1 %.0f; wave entry spread in a workgroup %.0f, wave 0 after first wave %.0f\n",
                                        static_cast<double>(h[24]) / h[23], static_cast<double>(h[25]) / h[23], static_cast<double>(h[26]) / h[23], static_cast<double>(h[27]) / h[23]);
+                    if (h[34]) fprintf(stderr, "hxt roles per block (cycles): compute wave 0 %.0f (waiting %.0f), loader 0 %.0f (waiting %.0f), n %llu\n",
+                                       static_cast<double>(h[30]) / h[34], static_cast<double>(h[32]) / h[34], static_cast<double>(h[31]) / h[34],
+                                       static_cast<double>(h[33]) / h[34], h[34]);
                     if (h[44]) fprintf(stderr, "hxq wave 0 (cycles): entry->barrier 1 %.0f, ->image %.0f, ->MFMA+stores issued %.0f, ->drained %.0f, n %llu\n",
                                        static_cast<double>(h[40]) / h[44], static_cast<double>(h[41]) / h[44], static_cast<double>(h[42]) / h[44],
                                        static_cast<double>(h[43]) / h[44], h[44]);

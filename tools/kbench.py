@@ -33,7 +33,7 @@ def run(env):
     if not line:
         return {"err": out.stderr[-500:]}
     d = json.loads(line[-1])
-    prof = [l for l in out.stderr.splitlines() if l.startswith("hxs")]
+    prof = [l for l in out.stderr.splitlines() if l.startswith(("hxs", "hxt", "hxq"))]
     if prof:
         d["prof"] = prof
     return d
