@@ -99,11 +99,15 @@ hipError_t hxtFmt(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 // row blocks one wave each; one remaining row block shared by 4 waves (every 4th period), two by
 // 2 waves each (every 2nd period), so waves w, w+4, w+8 -- one SIMD -- carry equal MFMA work.
 // Returns the compute wave count; *maxStride the largest period stride.
-static int hxtRoles(int nprog, int* role, int* maxStride) {
-    static const int knobRoles = std::getenv("GAR_HXT_ROLES") ? std::atoi(std::getenv("GAR_HXT_ROLES")) : 1;
+static int hxtRoles(int nprog, int NS, int* role, int* maxStride) {
+    // knob GAR_HXT_ROLES: 1 balanced, 0 one wave per row block; default balanced for NS >= 10 only
+    // (profiles/r04_ab: NS = 9 cfg2 0.125 ms one-per-row-block vs 0.145 balanced -- six loaders
+    // beside ten compute waves keep the ring ahead; NS = 10 cfg3 is the other way round)
+    static const int knobRoles = std::getenv("GAR_HXT_ROLES") ? std::atoi(std::getenv("GAR_HXT_ROLES")) : -1;
+    const bool balanced = knobRoles >= 0 ? knobRoles != 0 : NS >= 10;
     int w = 0;
     *maxStride = 1;
-    if (!knobRoles) {  // one wave per row block (hxs_kernel's mapping), six loaders beside ten compute waves
+    if (!balanced) {  // one wave per row block (hxs_kernel's mapping), six loaders beside ten compute waves
         for (int i = 0; i < nprog; ++i) role[w++] = i | (1 << 16);
         return w;
     }
@@ -229,14 +233,14 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     else vst = 0;
 
     // balanced kernel (hxt_kernel): f32 stereo frames or 16-channel rows in, f32 out (knob GAR_HXT=0: hxs_kernel)
-    // Default (knob unset): hxt_kernel for NS >= 10, where hxs_kernel's compute waves hold A (80 VGPRs)
-    // beside double-buffered accumulators and spill (cfg3 48k->44.1k Q32: 0.48 -> 0.36 ms); hxs_kernel
-    // below, where it is still the faster of the two (cfg2 / ns256, NS = 9).
+    // Default (knob unset): hxt_kernel wherever its load / store layouts apply -- after its loader spill
+    // fixes it beats hxs_kernel on every BASELINE plan (profiles/r04_ab: cfg2 0.125 vs 0.130 ms, ns256
+    // 1.81 vs 1.84 ms, cfg3 0.33 vs 0.46 ms); hxs_kernel keeps PCM, f64 and other layouts.
     static const int knobHxt = std::getenv("GAR_HXT") ? std::atoi(std::getenv("GAR_HXT")) : -1;
     int role[kHxtMaxComp] = {}, maxStride = 1, ncomp = 0;
-    const bool hxt = (knobHxt > 0 || (knobHxt < 0 && p.NS >= 10)) && !small && !od.pcm && !od.f64 && !src.in_pcm &&
+    const bool hxt = knobHxt != 0 && !small && !od.pcm && !od.f64 && !src.in_pcm &&
                      ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
-    if (hxt) ncomp = hxtRoles(p.nw, role, &maxStride);
+    if (hxt) ncomp = hxtRoles(p.nw, p.NS, role, &maxStride);
 
     int G = 0, R = 0, Rt = 0, Wg = 0;
     for (int pass = hxt && maxStride > 1 ? 0 : 1; pass < 2 && G == 0; ++pass) {  // hxt: G a multiple of the stride first

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 measurement call: all GPU tests, smoke, default bench line, rocprof kernel stats of the
 # same command, PMC of the streaming kernels (cfg2 hxs, ns256 hxs, cfg3 hxt), C-ABI short-call numbers.
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/r04final; mkdir -p $O
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/${FTAG:-r04final}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1
 s=$?; echo "PYTEST_EXIT $s" >> $O/gpu_tests.log; tail -2 $O/gpu_tests.log; [ $s -eq 0 ] || exit $s
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $O/smoke.log 2>&1
@@ -15,7 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pmc > $O/prof_bench.log 2>&1
 s=$?; echo "PROF_EXIT $s"; [ $s -eq 0 ] || exit $s
 cd $R
-TAG=r04_cfg2 WL=cfg2 KERNEL=hxs_kernel bash tools/pmc_hxs.sh || exit 1
-TAG=r04_ns256 WL=ns256 KERNEL=hxs_kernel bash tools/pmc_hxs.sh || exit 1
-TAG=r04_cfg3 WL=cfg3 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=r04b_cfg2 WL=cfg2 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=r04b_ns256 WL=ns256 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=r04b_cfg3 WL=cfg3 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
 exit 0
