@@ -559,8 +559,8 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
         achieved = algo_per_launch / launch_s / 1e9 if launches else None
         roof = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": PEAK_HBM_GBPS,
                 "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4) if achieved else None}
-        kernel_keys = ["hxs_kernel", "hx_kernel"]
-        kname = ("hxs_kernel / hx_kernel (fused DFTx2->polyphase banded FIR, f16-split "
+        kernel_keys = ["hxt_kernel", "hxs_kernel", "hx_kernel"]
+        kname = ("hxt_kernel / hxs_kernel / hx_kernel (fused DFTx2->polyphase banded FIR, f16-split "
                  "v_mfma_f32_16x16x32_f16, f32 accumulation)")
         algo_unit_bytes = algo_per_launch
     else:
