@@ -89,7 +89,7 @@ struct HxArgs {
 };
 
 // ---- staging ----------------------------------------------------------------
-// Fixed split scale: x * 2^kHxXs = xh + xl (f16).  Every |x| < kHxLoud keeps
+// Fixed split scale: x * 2^kHxXs = xh + xl (f16).  Every |x| < kHxLoud (just under 16) keeps
 // xh, xl finite, and the split of an element does not depend on its
 // neighbours -- the property that makes outputs chunk-invariant.  Elements
 // with !(|x| < kHxLoud) (Inf/NaN included) are staged as 0 and marked
@@ -99,7 +99,10 @@ struct HxArgs {
 // of a full-scale signal.
 constexpr int kHxXs = 12;
 constexpr int kHxLs = 11;
-constexpr float kHxLoud = 16.0f;
+// 16 - 2^-8 = 65520 / 2^12: the largest bound for which x * 2^12 rounds to a finite f16 (65520 itself
+// ties to even, i.e. to +Inf; with 16 here, |x| in [15.99609375, 16) staged hi = Inf and the MFMA
+// output was Inf/NaN).  The lo residual of every staged element is then <= 16 * 2^11, finite.
+constexpr float kHxLoud = 15.99609375f;
 
 // Image buffer layout: quad q (columns 4q..4q+3) at q*QS, QS = 16*Ws + 64: hi
 // rows (4 f16 = 8 B each) then lo rows; the +64 B skew puts the four quads of

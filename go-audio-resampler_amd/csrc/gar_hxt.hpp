@@ -39,7 +39,8 @@ __host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL)
 template <int NL>
 constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 constexpr int kHxtLdSlots = 8;                          // progress counters: ld[8] (loaders), cp[12] (compute)
-constexpr uint32_t kHxtLoudBits = 0x41800000u;          // bits(16.0f): |x| >= 16, Inf, NaN <=> (bits & 0x7fffffff) >= it
+constexpr uint32_t kHxtLoudBits = 0x417FF000u;          // bits(kHxLoud = 15.99609375f): !(|x| < kHxLoud) <=> (bits & 0x7fffffff) >= it
+static_assert(__builtin_bit_cast(uint32_t, kHxLoud) == kHxtLoudBits, "hxt's loud test must match hxLoud");
 
 struct HxtRole {
     int rb, ph, st;

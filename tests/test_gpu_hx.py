@@ -198,3 +198,26 @@ def test_hx_row16_small_launches_loud(gar, O, cuda, chunk):
         big = np.abs(np.asarray(want[c])) > 20
         assert big.any()
         assert np.max(np.abs(got[big, c] - want[c][big]) / np.abs(want[c][big])) <= 1e-6
+
+
+@pytest.mark.parametrize("chunks", [None, 4096])
+def test_hx_values_just_below_16(gar, O, cuda, chunks):
+    """Samples in [15.996, 16): x * 2^12 rounds to f16 +-Inf there (65520 ties to even), so the split
+    bound is 16 - 2^-8 -- at or above it a sample takes the exact path, just below it the split stays
+    finite.  Every output finite and within the float32 bar of the oracle, any chunking the same bits."""
+    n = 40000
+    x = signal(n, 2, 44100, seed=13).astype(np.float32).astype(np.float64)
+    vals = [15.99609375, 15.997, 15.9999, -15.99609375, -15.998, 15.996, -15.9960937, 15.99, 16.0]
+    rng = np.random.default_rng(3)
+    for i, v in enumerate(vals * 6):
+        x[int(rng.integers(100, n - 100)), i % 2] = v
+    x = x.astype(np.float32).astype(np.float64)
+    got = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32, None if chunks is None else chunk_sizes(n, chunks))
+    want = oracle_new(O, 44100, 48000, x, O.P_HIGH)
+    ex = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32_EXACT)
+    for c in range(2):
+        assert np.all(np.isfinite(got[:, c]))
+        assert rms(got[:, c], want[c]) <= max(3.0 * rms(ex[:, c], want[c]), F32_RMS_TOL)
+    if chunks is not None:
+        one = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
+        np.testing.assert_array_equal(got, one)
