@@ -39,6 +39,9 @@ __host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL)
 template <int NL>
 constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 constexpr int kHxtLdSlots = 8;                          // progress counters: ld[8] (loaders), cp[12] (compute)
+#ifndef GAR_HXT_UPUT
+#define GAR_HXT_UPUT 0
+#endif
 constexpr uint32_t kHxtLoudBits = 0x417FF000u;          // bits(kHxLoud = 15.99609375f): !(|x| < kHxLoud) <=> (bits & 0x7fffffff) >= it
 static_assert(__builtin_bit_cast(uint32_t, kHxLoud) == kHxtLoudBits, "hxt's loud test must match hxLoud");
 
@@ -209,7 +212,26 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
             // quad base recomputed per item (opaque): eight hoisted per-quad bases spill to VGPR lanes
             uint32_t qs = sh.QS;
             asm volatile("" : "+s"(qs));
+#if GAR_HXT_UPUT  // A/B: the mirror copy decided per 64-row piece (uniform) except at the mirror's end
+            if (row < nrow) {
+                char* qb = sh.ring + q * qs;
+                uint2 hv, lv;
+                hxSplit2(e[0], e[1], hv.x, lv.x);
+                hxSplit2(e[2], e[3], hv.y, lv.y);
+                *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
+                *reinterpret_cast<uint2*>(qb + dL + 8 * p) = lv;
+                constexpr int kPiece = FMT == 1 ? 64 : 16;
+                const int pLo = uni(p0 + kPiece * (FMT == 1 ? (lq + NL * k) >> 2 : lq + NL * k));  // piece's first ring row, unwrapped
+                const bool none = pLo >= mirror && pLo + kPiece <= R;  // uniform: no row of the piece in [0, mirror)
+                const bool all = pLo + kPiece <= mirror;               // uniform: every row of it
+                if (!none && (all || p < mirror)) {
+                    *reinterpret_cast<uint2*>(qb + 8 * (p + R)) = hv;
+                    *reinterpret_cast<uint2*>(qb + dL + 8 * (p + R)) = lv;
+                }
+            }
+#else
             if (row < nrow) hxtPut(sh.ring + q * qs, dL, p, R, mirror, e);
+#endif
         }
     }
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
