@@ -15,7 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pmc > $O/prof_bench.log 2>&1
 s=$?; echo "PROF_EXIT $s"; [ $s -eq 0 ] || exit $s
 cd $R
-TAG=r04b_cfg2 WL=cfg2 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
-TAG=r04b_ns256 WL=ns256 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
-TAG=r04b_cfg3 WL=cfg3 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=${PT:-r04b}_cfg2 WL=cfg2 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=${PT:-r04b}_ns256 WL=ns256 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
+TAG=${PT:-r04b}_cfg3 WL=cfg3 KERNEL=hxt_kernel bash tools/pmc_hxs.sh || exit 1
 exit 0
