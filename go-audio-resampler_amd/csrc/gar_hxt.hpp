@@ -42,6 +42,9 @@ constexpr int kHxtLdSlots = 8;                          // progress counters: ld
 #ifndef GAR_HXT_UPUT
 #define GAR_HXT_UPUT 0
 #endif
+#ifndef GAR_HXT_PKLOUD
+#define GAR_HXT_PKLOUD 0
+#endif
 constexpr uint32_t kHxtLoudBits = 0x417FF000u;          // bits(kHxLoud = 15.99609375f): !(|x| < kHxLoud) <=> (bits & 0x7fffffff) >= it
 static_assert(__builtin_bit_cast(uint32_t, kHxLoud) == kHxtLoudBits, "hxt's loud test must match hxLoud");
 
@@ -188,7 +191,7 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
     // (ten live row registers spill, and every reload's vmcnt(0) waits for the loads in flight)
     int ln = lane, lq = l;
     asm volatile("" : "+v"(ln), "+s"(lq));
-    uint32_t m = 0;
+    uint32_t m = 0, mh = 0;
 #pragma unroll
     for (int k = 0; k < hxtItems<NL>(); ++k) {
         int row, q;
@@ -206,7 +209,21 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
         }
         if (on) {  // uniform
             const f32x4 e = hxtItem<FMT, NL>(r, k);
+#if GAR_HXT_PKLOUD  // loud <=> the f16 hi half overflows (kHxLoud is exactly that bound): packed u16 max
+            {
+                uint32_t h0, l0, h1, l1;
+                hxSplit2(e[0], e[1], h0, l0);
+                hxSplit2(e[2], e[3], h1, l1);
+                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+                u16x2 mm = __builtin_bit_cast(u16x2, mh);
+                mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, h0 & 0x7fff7fffu));
+                mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, h1 & 0x7fff7fffu));
+                mh = __builtin_bit_cast(uint32_t, mm);
+                (void)l0; (void)l1;
+            }
+#else
             m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
+#endif
             int p = p0 + row;
             p = p >= R ? p - R : p;
             // quad base recomputed per item (opaque): eight hoisted per-quad bases spill to VGPR lanes
@@ -234,6 +251,9 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
 #endif
         }
     }
+#if GAR_HXT_PKLOUD
+    m = ((mh & 0xffffu) >= 0x7c00u || (mh >> 16) >= 0x7c00u) ? kHxtLoudBits : 0u;
+#endif
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
         hxtLoudLoad<FMT, NL>(hxsCold(), st, b, l, lane, sh);
 }
