@@ -165,6 +165,70 @@ def cpu_info():
     return model, os.cpu_count(), avail
 
 
+def cpu_quota():
+    """CPUs this process may keep busy: the cgroup CPU quota (cpu.max) if one is set, else None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, p = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(-(-int(q) // int(p))))
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        if q > 0:
+            return max(1, -(-q // p))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def rank_devices(world, rank, dev, dry):
+    """Every rank's process and device (all_gather_object over the process group when world > 1)."""
+    import socket
+    me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "host": socket.gethostname(),
+          "device": "dry-run (no GPU)" if dry else str(dev)}
+    if not dry:
+        import torch
+        me["device_name"] = torch.cuda.get_device_name(dev)
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
+def front_keys(line):
+    """The JSON line with the figures a reader (and the driver's parser) needs first: the contract's
+    keys, then the dominant kernel's per-launch time and roofline fraction, the streaming-call
+    figures and the CPU baseline, flat; everything else after them."""
+    roof = line.get("roofline") or {}
+    st = line.get("streaming") or {}
+    s256 = line.get("streaming_256ch") or {}
+    cpu = line.get("cpu_baseline") or {}
+    flat = {
+        "kernel_ms_per_launch": roof.get("kernel_ms_per_launch"),
+        "kernel_ms_min_median_max": roof.get("kernel_ms_min_median_max"),
+        "roofline_frac": roof.get("frac"),
+        "stream_dev_us_per_call": (st.get("device_api") or {}).get("us_per_call"),
+        "stream_host_us_per_call": (st.get("host_cabi") or {}).get("us_per_call"),
+        "stream_256ch_host_ms_per_call": s256.get("ms_per_call"),
+        "cpu_baseline_msamples_per_s": cpu.get("value"),
+        "cpu_baseline_cores": cpu.get("cores"),
+    }
+    head = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "rms_vs_oracle"]
+    out = {k: line[k] for k in head if k in line}
+    out.update({k: v for k, v in flat.items() if v is not None})
+    out.update({k: v for k, v in line.items() if k not in out})
+    return out
+
+
 def cpu_baseline(w, target_s=10.0):
     """The CPU restatement of the reference path (oracle/, 'port', AVX2 build) timed on
     the host: New(ir->orr, QualityX) Process+Flush per channel in float64 (the
@@ -195,8 +259,11 @@ def cpu_baseline(w, target_s=10.0):
     dt1 = run(x)
     one = frames * ch / dt1 / 1e6
     model, ncpu, avail = cpu_info()
-    threads = max(1, min(avail, 16))  # the GPU box's CPU share per GPU is 16
-    secs_t = max(probe, secs / 2)
+    quota = cpu_quota()
+    # every CPU this process may use (affinity), capped by a cgroup quota if one is set: the
+    # reference's EnableParallel runs a goroutine per channel on all cores (constant.go:223-249)
+    threads = max(1, min(avail, quota) if quota else avail)
+    secs_t = max(probe, min(secs / 2, secs * 8.0 / threads))  # bounded wall time however many threads
     fr_t = int(secs_t * w["ir"])
     xt = x[:fr_t]
     res = [0.0] * threads
@@ -212,13 +279,13 @@ def cpu_baseline(w, target_s=10.0):
         t.join()
     dtn = time.perf_counter() - t0
     alln = threads * fr_t * ch / dtn / 1e6
-    return {"value": round(one, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{secs:.1f} s of {ch}-ch {w['ir']}->{w['orr']} Quality{w['preset']} (New path, float64 "
-                      f"compute, oracle/ AVX2 build), Process+Flush, single thread, {dt1:.1f} s wall",
-            "all_cores": {"value": round(alln, 3), "cores": threads,
-                          "sample": f"{threads} threads x {secs_t:.1f} s independent {ch}-ch streams, "
-                                    f"{dtn:.1f} s wall"},
-            "cpu_model": model, "nproc": ncpu, "cpus_usable": avail}
+    return {"value": round(alln, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads x {secs_t:.1f} s independent {ch}-ch {w['ir']}->{w['orr']} "
+                      f"Quality{w['preset']} streams (New path, float64 compute, oracle/ AVX2 build), "
+                      f"Process+Flush per channel, {dtn:.1f} s wall",
+            "single_core": {"value": round(one, 3), "cores": 1,
+                            "sample": f"{secs:.1f} s of the same stream, one thread, {dt1:.1f} s wall"},
+            "cpu_model": model, "nproc": ncpu, "cpus_usable": avail, "cgroup_cpu_quota": quota}
 
 
 def pmc_traffic(args, workload, kernel_keys):
@@ -583,6 +650,10 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
     roof["launches_per_step_by_kind"] = {KIND_NAMES[k]: prof[k][1] / steps for k in prof if prof[k][1]}
     roof.update({"traffic": None, "kernel": kname, "kernel_kind": KIND_NAMES[dom],
                  "kernel_ms_per_launch": round(launch_s * 1e3, 5), "launches": launches})
+    try:  # spread of the per-launch event times behind the average
+        roof["kernel_ms_min_median_max"] = [round(v, 5) for v in r.profile_launch_stats(dom)]
+    except Exception:  # noqa: BLE001 -- an older library without the entry point
+        pass
     if algo_unit_bytes:
         roof["algo_hbm_bytes_per_launch"] = int(algo_unit_bytes)
         roof["algo_bytes_per_input_sample"] = round(algo_unit_bytes * per_step / (frames * C), 3)
@@ -623,9 +694,41 @@ def attach_traffic(obj, args, key, kernel_keys):
             roof["traffic_over_algo_uncorrected"] = round((traffic["read_bytes_uncorrected"] + traffic["write_bytes"]) / algo, 4)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` is authoritative.  Without a torchrun environment and N > 1, start N ranks (one
+    process per GPU) as a CHILD `torch.distributed.run` -- before this process touches the GPU --
+    and exit with its code; rank 0's JSON line reaches stdout through it.  Under torchrun, a
+    WORLD_SIZE that differs from --gpus is an error (a silent 1-rank run would report n_gpus 1).
+    Returns the world size this process runs with (or exits)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        n = args.gpus if args.gpus is not None else 1
+        if n > 1:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                   "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
+            env = dict(os.environ)
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+            env.setdefault("OMP_NUM_THREADS", "1")
+            p = subprocess.run(cmd, env=env)
+            sys.exit(p.returncode)
+        return 1
+    if args.gpus is not None and int(ws) != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}\n")
+        sys.exit(2)
+    return int(ws)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of one node; without torchrun, N > 1 starts N ranks itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
@@ -640,6 +743,7 @@ def main():
                     help="no GPU: dry-run handles (exact host state machine) over gloo -- the multi-rank "
                          "sharding and reduction end to end on CPU (tests/test_dist.py)")
     args = ap.parse_args()
+    launch_ranks(args, sys.argv[1:])
 
     world, rank, local = dist_env()
     dev = None
@@ -657,12 +761,16 @@ def main():
             torch.cuda.set_device(0)
         dev = torch.device("cuda", torch.cuda.current_device())
 
+    ranks = rank_devices(world, rank, dev, args.dry_run)
     line, keys = run_workload(args.workload, args, args.steps, args.warmup, world, rank, dev, primary=True)
+    line["ranks"] = ranks
     if rank == 0 and world == 1 and not args.no_pmc and not args.dry_run:
         attach_traffic(line, args, args.workload, keys)
     line["cpu_baseline"] = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         line["cpu_baseline"] = cpu_baseline(WORKLOADS[args.workload])
+    if rank == 0 and world == 1 and not args.no_streaming and not args.dry_run and args.workload == "cfg2":
+        line["streaming_256ch"] = time_streaming_host(WORKLOADS["ns256"], dev)
     sec = (secondary_default(args.workload, world) if args.secondary == "auto"
            else [] if args.secondary == "none" else [k for k in args.secondary.split(",") if k])
     if sec:
@@ -676,7 +784,7 @@ def main():
     if args.dry_run:
         line["dry_run"] = True
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(front_keys(line)), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
@@ -769,6 +877,44 @@ def time_streaming(gar, torch, w, x, C, dev, seconds=60.0):
                       "sample": f"{hs:.0f} s, gar_process_multi_f64 per chunk from planar float64 host buffers "
                                 "(H2D + launches + D2H + synchronise per call, PCIe-inclusive)"},
     }
+
+
+def time_streaming_host(w, dev, calls=40, chunk=4096):
+    """The 256-channel drop-in call of the north-star geometry through the host C-ABI: one
+    gar_process_multi_f64 per 4096-frame chunk from planar float64 host buffers (H2D + launch +
+    D2H + synchronise inside every call, what a cgo caller of ProcessMulti gets), after a warm-up
+    pass.  Bounded sample: `calls` calls."""
+    import ctypes as Ct
+    import gar
+    C = w["ch"]
+    frames = calls * chunk
+    x = synth_stream(frames, C, 99, w["ir"]).astype(np.float64)
+    xh = [np.ascontiguousarray(x[:, c]) for c in range(C)]
+    r = gar.New(gar.Config(w["ir"], w["orr"], C, getattr(gar, "Quality" + w["preset"]), ComputeDtype=gar.F32,
+                           Device=dev.index))
+    cap = int(chunk * w["orr"] / w["ir"]) + 64
+    outs = [np.empty(cap) for _ in range(C)]
+    outp = (Ct.c_void_p * C)(*[o.ctypes.data for o in outs])
+    counts = np.zeros(C, dtype=np.int64)
+    L = gar.lib()
+    args = [((Ct.c_void_p * C)(*[a.ctypes.data + 8 * s for a in xh]), min(chunk, frames - s))
+            for s in range(0, frames, chunk)]
+
+    def host_pass():
+        r.Reset()
+        for inp, n in args:
+            st = L.gar_process_multi_f64(r._h, inp, C, n, outp, cap, counts.ctypes.data)
+            if st != 0:
+                raise RuntimeError(f"gar_process_multi_f64: {st}")
+
+    host_pass()
+    t0 = time.perf_counter()
+    host_pass()
+    dt = time.perf_counter() - t0
+    return {"channels": C, "chunk_frames": chunk, "calls": len(args), "ms_per_call": round(dt / len(args) * 1e3, 4),
+            "value": round(frames * C / dt / 1e6, 2), "unit": "Msamples/s",
+            "sample": f"{len(args)} calls of {chunk} frames x {C} ch {w['ir']}->{w['orr']} Quality{w['preset']}, "
+                      "gar_process_multi_f64 from planar float64 host buffers (PCIe-inclusive)"}
 
 
 if __name__ == "__main__":

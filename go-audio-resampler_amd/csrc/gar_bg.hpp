@@ -682,8 +682,9 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
         }
         __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
     }
-    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;  // the first row block of this workgroup
-    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
+    // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
+    // no second pass); a workgroup without one copies it here
+    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
 }
 
 // Small launches of row-block-aligned plans, column blocks as bg_rb_kernel (16 consecutive columns,
@@ -784,8 +785,9 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rc_kernel(BgDev p, SrcD
         }
         __syncthreads();  // window and slots free for the next (column block, row block)
     }
-    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;
-    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);
+    // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
+    // no second pass); a workgroup without one copies it here
+    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
 }
 
 template <class TC, int NS>

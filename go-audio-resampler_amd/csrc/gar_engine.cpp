@@ -628,7 +628,12 @@ struct gar_resampler {
     // a HIP failure mid-call may leave counters advanced past the histories: refuse
     // further work until Reset (ADVICE: no silent wrong output)
     bool poisoned = false;
-    hipStream_t failStream = nullptr;  // the stream of the call that poisoned the handle
+    hipEvent_t failEv = nullptr;  // recorded on the failing call's stream (the caller may destroy that stream)
+    bool failEvValid = false;
+    // device status word (pinned, host-mapped): a kernel that detects a broken invariant of its own
+    // (hxt_kernel: an expired progress wait) writes a nonzero code; every ABI call checks it first
+    int* errHost = nullptr;
+    int* errDev = nullptr;
     gar_config cfg{};
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
@@ -643,6 +648,7 @@ struct gar_resampler {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evPool;
     double profiledMs[6] = {0, 0, 0, 0, 0, 0};
     int64_t profiledLaunches[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<float> launchMs[6], readMs[6];  // per-launch ms since the last read / of the last read
 };
 
 namespace gar {
@@ -709,8 +715,11 @@ SrcDesc mkSrc(const Hist& hs, int C, int64_t x0, const InView& in) {
     return s;
 }
 
+thread_local int* g_curErr = nullptr;  // device status word of the handle whose call is running (callOn)
+
 OutDesc mkOut(const OutView& o, int64_t o0, int64_t n) {
     OutDesc d{};
+    d.err = g_curErr;
     d.out = o.p;
     d.o0 = o0;
     d.fs = o.fs;
@@ -1200,12 +1209,32 @@ gar_status wrap(F&& f) {
 // One ABI call that touches the device: handle's device current, ordered after
 // the handle's previous call (any stream), recorded for the next; a device
 // error poisons the handle until Reset.
+// A kernel of an earlier (asynchronous) call raised the handle's device status word: the outputs of
+// that call are not the reference's, so the handle is poisoned until Reset (no silent wrong output).
+bool devFault(Handle* h) {
+    if (!h->errHost) return false;
+    const int v = __atomic_load_n(h->errHost, __ATOMIC_ACQUIRE);
+    if (!v) return false;
+    h->poisoned = true;
+    g_err = std::string("device error reported by hxt_kernel: ") +
+            (v == kHxtErrLoadWait ? "a compute wave's LDS load-progress wait expired"
+                                  : (v == kHxtErrSlotWait ? "a loader's LDS ring-slot wait expired" : "unknown code")) +
+            " (code " + std::to_string(v) + "); outputs of the launch are invalid; call Reset";
+    return true;
+}
+
 template <class F>
 gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
     if (h->poisoned) return guard(GAR_ERR_DEVICE, "handle unusable after an earlier device error; call Reset");
     if (h->dry) return wrap(f);
+    if (devFault(h)) return GAR_ERR_DEVICE;
     DeviceGuard dg(h->device);
-    const gar_status st = wrap([&]() -> gar_status {
+    struct ErrScope {  // the kernels launched by this call report into this handle's status word
+        int* prev;
+        explicit ErrScope(int* e) : prev(g_curErr) { g_curErr = e; }
+        ~ErrScope() { g_curErr = prev; }
+    } es(h->errDev);
+    gar_status st = wrap([&]() -> gar_status {
         if (h->orderValid && h->lastStream != s) HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
         const gar_status r = f();
         if (hostSynced) {  // the call synchronised its stream: nothing of it is left to order after
@@ -1219,7 +1248,10 @@ gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
     });
     if (st == GAR_ERR_DEVICE || (st == GAR_ERR_INVALID_ARGUMENT && g_launchLimit)) {  // state may be half-updated
         h->poisoned = true;
-        h->failStream = s;
+        // drained by Reset through an event: the caller may destroy `s` after the failed call
+        h->failEvValid = h->failEv && hipEventRecord(h->failEv, s) == hipSuccess;
+    } else if (st == GAR_OK && hostSynced && devFault(h)) {  // this call's own kernels reported
+        st = GAR_ERR_DEVICE;
     }
     return st;
 }
@@ -1280,6 +1312,16 @@ gar_status initDevice(Handle* h) {
     // device (host visibility of results goes through the stream syncs of the host paths); a
     // system-scope release would write back every dirty L2 line after each call
     HIPCHK(hipEventCreateWithFlags(&h->orderEv, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&h->failEv, hipEventDisableTiming));
+    // the device status word: coherent pinned host memory, so a kernel's system-scope store is seen by
+    // the next ABI call without a synchronisation
+    void* w = nullptr;
+    HIPCHK(hipHostMalloc(&w, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    h->errHost = static_cast<int*>(w);
+    *h->errHost = 0;
+    void* d = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&d, w, 0));
+    h->errDev = static_cast<int*>(d);
     return GAR_OK;
 }
 
@@ -1540,10 +1582,30 @@ void gar_free(gar_resampler* r) {
         }
         r->groups.clear();
         r->stages.clear();
+        if (r->failEv) (void)hipEventDestroy(r->failEv);
+        if (r->errHost) (void)hipHostFree(r->errHost);
         if (r->stream) (void)hipStreamDestroy(r->stream);
     } catch (...) {
     }
     delete r;
+}
+
+gar_status gar_synchronize(gar_resampler* r) {
+    if (!r) return GAR_ERR_INVALID_ARGUMENT;
+    if (r->dry) return GAR_OK;
+    DeviceGuard dg(r->device);
+    const gar_status st = wrap([&]() -> gar_status {
+        if (r->orderValid) HIPCHK(hipEventSynchronize(r->orderEv));
+        if (r->stream) HIPCHK(hipStreamSynchronize(r->stream));
+        return GAR_OK;
+    });
+    if (st != GAR_OK) {
+        r->poisoned = true;
+        return st;
+    }
+    if (devFault(r)) return GAR_ERR_DEVICE;
+    if (r->poisoned) return guard(GAR_ERR_DEVICE, "handle unusable after an earlier device error; call Reset");
+    return GAR_OK;
 }
 
 int64_t gar_estimate_output(const gar_resampler* r, int64_t n) { return r ? estimate(r, n) : -1; }
@@ -1822,18 +1884,22 @@ void gar_reset(gar_resampler* r) {
     if (!r) return;
     DeviceGuard dg(r->dry ? -1 : r->device);
     try {
+        if (!r->dry) (void)devFault(r);  // a raised status word takes the recovery path (and is cleared there)
         if (r->poisoned) {  // recover: drain the handle's streams, fresh state
             // the failing call recorded no order event, and launches it already queued on its
             // caller stream may still read the histories and scratch freed below: drain that stream
-            // (only the streams this handle enqueued on -- never the whole device)
-            (void)hipStreamSynchronize(r->failStream);
+            // (only the streams this handle enqueued on -- never the whole device; the failing call's
+            // stream through the event recorded on it, since the caller may have destroyed it)
+            if (r->failEvValid) (void)hipEventSynchronize(r->failEv);
             if (r->stream) (void)hipStreamSynchronize(r->stream);
             if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
             (void)hipGetLastError();
+            if (r->errHost) __atomic_store_n(r->errHost, 0, __ATOMIC_RELEASE);  // every launch that could write it has drained
             r->groups.clear();
             r->groups.push_back(freshGroup(r, 0, r->channels));
             r->poisoned = false;
-            r->failStream = nullptr;
+            r->failEvValid = false;
+            r->orderValid = false;
             return;
         }
         // one group over every channel: reset in place, keeping its device buffers
@@ -1979,6 +2045,7 @@ gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t*
             HIPCHK(hipEventElapsedTime(&t, ev.a, ev.b));
             r->profiledMs[ev.tag] += t;
             r->profiledLaunches[ev.tag] += 1;
+            r->launchMs[ev.tag].push_back(t);
             r->evPool.emplace_back(ev.a, ev.b);
         }
         r->events.clear();
@@ -1986,8 +2053,27 @@ gar_status gar_profile_read(gar_resampler* r, int32_t kind, double* ms, int64_t*
         if (launches) *launches = r->profiledLaunches[kind];
         r->profiledMs[kind] = 0;
         r->profiledLaunches[kind] = 0;
+        r->readMs[kind].swap(r->launchMs[kind]);
+        r->launchMs[kind].clear();
         return GAR_OK;
     });
+}
+
+gar_status gar_profile_launch_stats(gar_resampler* r, int32_t kind, double* min_ms, double* median_ms, double* max_ms) {
+    if (!r || kind < 0 || kind > 5) return GAR_ERR_INVALID_ARGUMENT;
+    std::vector<float> v = r->readMs[kind];
+    if (v.empty()) {
+        if (min_ms) *min_ms = 0;
+        if (median_ms) *median_ms = 0;
+        if (max_ms) *max_ms = 0;
+        return GAR_OK;
+    }
+    std::sort(v.begin(), v.end());
+    const size_t n = v.size();
+    if (min_ms) *min_ms = v.front();
+    if (max_ms) *max_ms = v.back();
+    if (median_ms) *median_ms = n % 2 ? v[n / 2] : 0.5 * (static_cast<double>(v[n / 2 - 1]) + v[n / 2]);
+    return GAR_OK;
 }
 
 gar_status gar_design_engine(double in_rate, double out_rate, int32_t q, gar_engine_geometry* geom, double* dft,

@@ -137,8 +137,10 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 }
 }  // namespace
 
-// LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag (256 B).
-static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 256; }
+// LDS bytes of an hxs launch: ring (four quads of hi + lo rows), loud ranges + flag, hxt_kernel's
+// progress counters (kHxtSyncOff + kHxtSyncBytes, rounded up).
+static_assert(kHxtSyncOff + kHxtSyncBytes <= 320, "hxt progress counters past the reserved LDS");
+static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 320; }
 
 // Ring geometry of G periods per group: R ring rows, Rt rows incl. the mirror (rounded to 16 so
 // the quad stride 16*Rt + 64 is 64 mod 256 B: the four quads of a transposed read land on
@@ -238,23 +240,36 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     // 1.81 vs 1.84 ms, cfg3 0.33 vs 0.46 ms); hxs_kernel keeps PCM, f64 and other layouts.
     static const int knobHxt = std::getenv("GAR_HXT") ? std::atoi(std::getenv("GAR_HXT")) : -1;
     int role[kHxtMaxComp] = {}, maxStride = 1, ncomp = 0;
-    const bool hxt = knobHxt != 0 && !small && !od.pcm && !od.f64 && !src.in_pcm &&
-                     ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
+    bool hxt = knobHxt != 0 && !small && !od.pcm && !od.f64 && !src.in_pcm &&
+               ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
     if (hxt) ncomp = hxtRoles(p.nw, p.NS, role, &maxStride);
 
     int G = 0, R = 0, Rt = 0, Wg = 0;
-    for (int pass = hxt && maxStride > 1 ? 0 : 1; pass < 2 && G == 0; ++pass) {  // hxt: G a multiple of the stride first
-        for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
-            int r, rt, wg;
-            hxsRingFor(p, cand, r, rt, wg);
-            if (cand > 1 && cand > Np) continue;
-            if (knobG > 0 && cand > knobG && cand > 1) continue;
-            if (!hxsRingFits(p, cand, rt)) continue;
-            if (hxt && cand * Qc > hxtMaxRows(ncomp + 6 <= kHxtWaves ? 6 : 4)) continue;
-            if (pass == 0 && cand % maxStride != 0) continue;
-            G = cand; R = r; Rt = rt; Wg = wg;
-            break;
+    auto pickG = [&]() {
+        for (int pass = hxt && maxStride > 1 ? 0 : 1; pass < 2 && G == 0; ++pass) {  // hxt: G a multiple of the stride first
+            for (int cand = small ? 1 : kHxsMaxG; cand >= 1; --cand) {
+                int r, rt, wg;
+                hxsRingFor(p, cand, r, rt, wg);
+                if (cand > 1 && cand > Np) continue;
+                if (knobG > 0 && cand > knobG && cand > 1) continue;
+                if (!hxsRingFits(p, cand, rt)) continue;
+                if (hxt && cand * Qc > hxtMaxRows(ncomp + 6 <= kHxtWaves ? 6 : 4)) continue;
+                // hxt: a producer runs at most (ring slots + 2) loads / groups ahead of the slowest one,
+                // which the arrival slots must cover (gar_hxt.hpp progress counters)
+                if (hxt && r / (cand * static_cast<int>(Qc)) + 3 > kHxtSlots) continue;
+                if (pass == 0 && cand % maxStride != 0) continue;
+                G = cand; R = r; Rt = rt; Wg = wg;
+                break;
+            }
         }
+    };
+    pickG();
+    if (G == 0 && hxt) {  // no group size fits hxt_kernel's limits: hxs_kernel's
+        hxt = false;
+        ncomp = 0;
+        maxStride = 1;
+        for (int& r : role) r = 0;
+        pickG();
     }
     if (G == 0) return hipErrorNotSupported;
 
@@ -301,6 +316,19 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.vst = vst;
     x.ncomp = ncomp;
     for (int w = 0; w < kHxtMaxComp; ++w) x.role[w] = role[w];
+    // progress-wait bound and the device status word; development knob GAR_HXT_FAULT=1 (read per
+    // launch, so one test process can set it) makes the compute waves' load count unreachable
+    // and the bound short: the launch must end with GAR_ERR_DEVICE, not with output
+    x.err = od.err;
+    x.pollMax = 1 << 24;
+    x.faultNeed = 0;
+    if (hxt) {
+        const char* f = std::getenv("GAR_HXT_FAULT");
+        if (f && f[0] == '1') {
+            x.pollMax = 1 << 12;
+            x.faultNeed = 1 << 28;
+        }
+    }
     x.src = src;
     x.od = od;
     x.rows = p.rows;

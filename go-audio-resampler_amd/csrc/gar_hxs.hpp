@@ -20,7 +20,7 @@
 //    rows, so every group's window is contiguous), so each input row is staged
 //    once per column instead of once per G-period window (round-1 kernel:
 //    W/(G*Qc) = 1.34x; here (Np*Qc + Kread - Qc)/(Np*Qc) ~ 1.02x).
-//  * Loud elements (|x| >= 16, Inf, NaN) are staged as zero and their
+//  * Loud elements (!(|x| < kHxLoud): |x| >= 16 - 2^-8, Inf, NaN) are staged as zero and their
 //    column-relative row range recorded; after the block, every output whose
 //    window holds one is recomputed exactly (hxExactT: f64, two stages when
 //    non-finite) by the same workgroup.
@@ -105,6 +105,9 @@ struct HxsArgs {
     // p % stride == phase (phase = (role[w] >> 8) & 0xff, stride = role[w] >> 16)
     int ncomp;
     int role[12];
+    int* err;               // the handle's device status word (host-mapped), written when a progress wait expires
+    int pollMax;            // progress-wait bound in polls (2^24; development knob GAR_HXT_FAULT: 2^12)
+    int faultNeed;          // development (GAR_HXT_FAULT=1): added to the compute waves' load count, unreachable
     // hxq_kernel (small f32 STEREO / ROW16 launches): workgroup = (block, qRbs row blocks), qGroups per block
     int qRbs, qGroups;
     int qU0[12], qRbw[12];  // first window row / row block of each row-block program (HxDev::hU0)

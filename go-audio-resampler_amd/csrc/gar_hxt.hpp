@@ -38,7 +38,6 @@ __host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL)
 // FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row).
 template <int NL>
 constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
-constexpr int kHxtLdSlots = 8;                          // progress counters: ld[8] (loaders), cp[12] (compute)
 #ifndef GAR_HXT_UPUT
 #define GAR_HXT_UPUT 0
 #endif
@@ -259,46 +258,69 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
 }
 
 // ---- progress counters (LDS) -------------------------------------------------------------
-// Inside a block no workgroup barrier is taken: loader l publishes ld[l] = loads converted, compute
-// wave w publishes cp[w] = groups finished.  Group g may run once every loader has converted loads
-// 0 .. P+g-1 (its window); load j may overwrite ring rows once every compute wave has finished the
-// last group whose window held them.  A wave publishes after s_waitcnt lgkmcnt(0) (its ring writes
-// / reads done), and LDS executes one wave's operations in order, so a reader that sees the count
-// and then reads the ring sees the data.  Waits are bounded (a wrong count ends the wait after
-// ~2^24 polls with wrong output instead of a hung GPU).
-typedef int i32x4v __attribute__((ext_vector_type(4)));
+// Inside a block no workgroup barrier is taken.  Two monotone counters carry the hand-offs:
+// ldDone = loads converted by EVERY loader, cpDone = groups finished by EVERY compute wave.
+// Group g may run once ldDone >= P+g (its window, loads 0 .. P+g-1); load j may overwrite ring
+// rows once cpDone reaches the last group whose window held them (hxtFreeNeed).
+// Each counter is advanced by the last of its producers to arrive: a producer that is done with
+// load j / group g adds 1 to the arrival slot arr[j % kHxtSlots] (ds_add_rtn, lane 0 only) and the
+// one that completes the count writes done = j + 1.  Producers finish their items in order, so the
+// last arrival at j also means every producer is done with everything before j, and `done` only
+// grows.  A producer can run at most (ring slots + 2) loads / groups ahead of the slowest one
+// (host check hxtSlotsOk), so slot j % kHxtSlots never holds arrivals of two laps at once.
+// A producer arrives after s_waitcnt lgkmcnt(0) (its ring writes / reads done), and LDS executes
+// one wave's operations in order, so a waiter that sees `done` and then reads the ring sees the
+// data.  A waiter polls one dword (broadcast ds_read_b32, s_sleep backoff) -- round 4 polled
+// every producer's own counter with two or three ds_read_b128 per poll.
+// Waits are bounded (x.pollMax polls): an expired wait means a counting bug, so the wave records
+// it in the workgroup's abort word (every later wait of the workgroup returns at once, the grid
+// drains) and in the handle's device status word x.err (host-mapped; the C-ABI reports
+// GAR_ERR_DEVICE naming hxt_kernel and refuses the handle until Reset) -- never silent output.
 typedef __attribute__((address_space(3))) int lds_i32;
-typedef __attribute__((address_space(3))) i32x4v lds_i32x4;
+constexpr int kHxtSlots = 16;                            // arrival slots per direction
 // Explicit LDS pointers: a generic pointer makes the polls flat loads, and a flat load's
 // s_waitcnt vmcnt(0) waits for every store the wave has in flight.
 struct HxtSync {
-    lds_i32* ld;  // [kHxtLdSlots]
-    lds_i32* cp;  // [kHxtMaxComp]
+    lds_i32* ldArr;   // [kHxtSlots] loader arrivals per load
+    lds_i32* cpArr;   // [kHxtSlots] compute-wave arrivals per group
+    lds_i32* ldDone;  // loads converted by every loader
+    lds_i32* cpDone;  // groups finished by every compute wave
+    lds_i32* abort;   // a wait of this workgroup expired (sticky for the launch)
 };
+// LDS bytes past loudLo (hxsLds reserves them): loudLo[16], loudHi[16], flag, then the counters
+constexpr int kHxtSyncOff = 160;
+constexpr int kHxtSyncBytes = 4 * (2 * kHxtSlots + 3);
 
-__device__ __forceinline__ void hxtPublish(lds_i32* slot, int v, int lane) {
+// Producer arrival for item j (load or group) of `n` producers.
+__device__ __forceinline__ void hxtArrive(lds_i32* arr, lds_i32* done, int j, int n, int lane) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring writes / reads done
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) *reinterpret_cast<volatile lds_i32*>(slot) = v;
+    if (lane == 0) {
+        const int prev = __hip_atomic_fetch_add(arr + (j & (kHxtSlots - 1)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (prev == (j / kHxtSlots) * n + n - 1) *reinterpret_cast<volatile lds_i32*>(done) = j + 1;
+    }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// min(cnt[0 .. n)) >= need, n <= 12 (16-B aligned counters, read as int4).
-__device__ __forceinline__ void hxtWait(const lds_i32* cnt, int n, int need) {
-    for (int it = 0; it < (1 << 24); ++it) {
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        const i32x4v a = *reinterpret_cast<const volatile lds_i32x4*>(cnt);
-        int m = min(min(a.x, a.y), min(a.z, a.w));
-        if (n > 4) {
-            const i32x4v b = *reinterpret_cast<const volatile lds_i32x4*>(cnt + 4);
-            m = min(m, min(min(b.x, b.y), min(b.z, b.w)));
-        }
-        if (n > 8) {
-            const i32x4v c = *reinterpret_cast<const volatile lds_i32x4*>(cnt + 8);
-            m = min(m, min(min(c.x, c.y), min(c.z, c.w)));
-        }
-        if (m >= need) break;
+// *done >= need, bounded; on expiry the abort word and the handle's status word are set.
+__device__ __forceinline__ void hxtWait(const HxsArgs& x, const HxtSync& sy, const lds_i32* done, int need, int code,
+                                        int lane) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (*reinterpret_cast<const volatile lds_i32*>(done) >= need) return;  // the common case: one read
+    if (*reinterpret_cast<const volatile lds_i32*>(sy.abort)) return;      // after an expiry: no more waiting
+    const int pmax = x.pollMax;
+    int it = 0;
+    for (; it < pmax; ++it) {
         __builtin_amdgcn_s_sleep(1);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (*reinterpret_cast<const volatile lds_i32*>(done) >= need) break;
+        if (*reinterpret_cast<const volatile lds_i32*>(sy.abort)) { it = pmax; break; }
+    }
+    if (it >= pmax) {  // expired (here or in another wave of the workgroup): record, stop waiting
+        if (lane == 0) {
+            *reinterpret_cast<volatile lds_i32*>(sy.abort) = 1;
+            if (x.err) __hip_atomic_store(x.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
@@ -351,7 +373,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (j >= P) {
                     if (j == P) p0 = Wg;  // Wg < R
                     need = last < 0 ? 0 : need + 1;
-                    if (need > 0 && !(dbg & 64)) hxtWait(sy.cp, x.ncomp, need);  // development 64: loaders never wait
+                    if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpDone, need, kHxtErrSlotWait, lane);  // development 64: loaders never wait
                     last += GQ;
                 }
                 if (!((dbg & 16) && j >= P)) {
@@ -359,7 +381,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                     if (fastL[d]) hxtConvert<FMT, NL>(x, st, uni(p0), buf[d], b, l, lane, sh);
                     else hxtGatherLoad(xp, st, b, l, NL, lane, sh);
                 }
-                hxtPublish(sy.ld + l, j + 1, lane);
+                hxtArrive(sy.ldArr, sy.ldDone, j, NL, lane);
                 p0 += GQ;
                 if (p0 >= R) p0 -= R;
             }
@@ -411,7 +433,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         while (first < p0) first += ro.st;
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
-            if (!(dbg & 32)) hxtWait(sy.ld, kHxtLdSlots, P + g);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
+            if (!(dbg & 32)) hxtWait(x, sy, sy.ldDone, P + g + x.faultNeed, kHxtErrLoadWait, lane);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
             // the lane's ring offset, recomputed per group (a value held across the group loop spills,
             // and its reload's vmcnt(0) would wait for this wave's output stores)
             int ln = lane;
@@ -448,7 +470,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
                 aH = aN;
             }
         }
-        hxtPublish(sy.cp + wt, g + 1, lane);  // this wave's reads of group g's window are done
+        hxtArrive(sy.cpArr, sy.cpDone, g, x.ncomp, lane);  // this wave's reads of group g's window are done
     }
 }
 
@@ -504,12 +526,16 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     s.loudHi = s.loudLo + 16;
     s.flag = s.loudHi + 16;
     HxtSync sy;
-    // 160 B past loudLo: ld[8], cp[12] (hxsLds reserves 256 B past the ring)
-    sy.ld = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + 160);
-    sy.cp = sy.ld + kHxtLdSlots;
+    // kHxtSyncOff B past loudLo (hxsLds reserves the space past the ring): arrival slots, done counters, abort
+    sy.ldArr = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + kHxtSyncOff);
+    sy.cpArr = sy.ldArr + kHxtSlots;
+    sy.ldDone = sy.cpArr + kHxtSlots;
+    sy.cpDone = sy.ldDone + 1;
+    sy.abort = sy.cpDone + 1;
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
     const bool comp = wt < x.ncomp;
+    if (threadIdx.x == 0) *sy.abort = 0;  // sticky for the launch (ordered by the first block's barriers)
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
         __syncthreads();  // the previous block's ring reads and fixup done
@@ -517,11 +543,8 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
             s.loudLo[threadIdx.x] = INT_MAX;
             s.loudHi[threadIdx.x] = -1;
         }
-        if (threadIdx.x < kHxtLdSlots + kHxtMaxComp) {  // ld[8], cp[12]; unused slots never hold back a wait
-            const int i = threadIdx.x;
-            sy.ld[i] = (i < kHxtLdSlots ? i >= NL : i - kHxtLdSlots >= x.ncomp) ? INT_MAX : 0;
-        }
-        if (threadIdx.x == 16) *s.flag = 0;
+        if (threadIdx.x < 2 * kHxtSlots + 2) sy.ldArr[threadIdx.x] = 0;  // arrivals, ldDone, cpDone
+        if (threadIdx.x == 64) *s.flag = 0;
         __syncthreads();
         if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane);
         else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane);

@@ -31,6 +31,7 @@ struct OutDesc {
     int f64;
     int pcm;               // 0 float output, else PCM bits (int(clamp(y, -1, 1) * maxVal))
     int64_t o_lo, o_hi;
+    int* err;              // the calling handle's device status word (host-mapped), null if none
 };
 
 // Integer PCM <-> float, after cmd/resample-wav/main.go:444-543 (maxInt16/24/32, main.go:54-56):
@@ -51,6 +52,11 @@ __host__ __device__ inline void pcmWrite(void* p, int64_t e, int bits, double y)
 }
 
 struct HxDev;
+
+// Device status codes a kernel writes into the handle's status word (OutDesc::err):
+// hxt_kernel (gar_hxt.hpp hxtWait) -- 1 a compute wave's load-progress wait expired, 2 a loader's
+// ring-slot wait expired.
+constexpr int kHxtErrLoadWait = 1, kHxtErrSlotWait = 2;
 
 // A launch whose configuration the device cannot run (dynamic LDS above the kernel's limit): the
 // launcher records what was exceeded here and returns hipErrorInvalidConfiguration; the C-ABI turns
@@ -82,7 +88,7 @@ struct HxDev {
     const void* A;       // [nw][kch*NS][2][64][8] f16
     const int* progs;    // [nw][kBgProgInts] (HxPlan::progTable)
     const int* reds;     // [nred][kBgRedInts]
-    // exact fallback of outputs whose windows hold |x| >= 16 / Inf / NaN
+    // exact fallback of outputs whose windows hold a loud element: !(|x| < kHxLoud = 16 - 2^-8), Inf, NaN
     const double* rows;  // [Pc][rowMax] FIR rows (f64)
     const int* rowOff;   // [Pc]
     const int* rowLen;   // [Pc]

@@ -90,6 +90,7 @@ EXPORTED = [
     "gar_device_flush_size", "gar_reset", "gar_get_ratio", "gar_get_latency", "gar_get_info", "gar_channels",
     "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite", "gar_profile_enable",
     "gar_profile_read", "gar_stage_state", "gar_num_stages", "gar_stage_geometry", "gar_get_statistics",
+    "gar_synchronize", "gar_profile_launch_stats",
 ]
 
 _lib = None
@@ -151,6 +152,8 @@ def lib():
         "gar_num_stages": (i32, [vp]),
         "gar_stage_geometry": (i32, [vp, i32, C.POINTER(d), C.POINTER(EngineGeometry)]),
         "gar_get_statistics": (i32, [vp, i32, C.POINTER(i64), C.POINTER(i64)]),
+        "gar_synchronize": (i32, [vp]),
+        "gar_profile_launch_stats": (i32, [vp, i32, C.POINTER(d), C.POINTER(d), C.POINTER(d)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -305,6 +308,17 @@ class Resampler:
         ms, n = C.c_double(0), C.c_int64(0)
         _check(lib().gar_profile_read(self._h, kind, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def profile_launch_stats(self, kind=0):
+        """(min, median, max) ms per launch of the launches the last profile_read(kind) summed."""
+        a, b, c = C.c_double(0), C.c_double(0), C.c_double(0)
+        _check(lib().gar_profile_launch_stats(self._h, kind, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+    def synchronize(self):
+        """Wait for the handle's enqueued device work; raises ResamplerError (GAR_ERR_DEVICE) when a
+        kernel reported a broken invariant (gar.h gar_synchronize)."""
+        _check(lib().gar_synchronize(self._h))
 
     def num_stages(self):
         return lib().gar_num_stages(self._h)

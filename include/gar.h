@@ -183,6 +183,14 @@ gar_status gar_flush_device(gar_resampler *r, int32_t channels, void *out, int32
 /* Exact lockstep output sizes (-1 if channels are not in lockstep). */
 int64_t gar_device_output_size(const gar_resampler *r, int64_t frames);
 int64_t gar_device_flush_size(const gar_resampler *r);
+/* Waits until every call enqueued on the handle has run and reports how it ended: GAR_OK, or
+ * GAR_ERR_DEVICE when a kernel of one of them reported a broken invariant into the handle's
+ * device status word (e.g. an expired progress wait of the streaming kernel: its outputs are
+ * invalid) or a HIP error occurred; the handle then refuses work until gar_reset.  Every ABI call
+ * also checks the status word on entry, and the host-memory calls (which synchronise) after their
+ * own kernels.  No Go counterpart: the reference's calls are synchronous (constant.go:88-146); this
+ * is the synchronisation point of the asynchronous *_device entry points. */
+gar_status gar_synchronize(gar_resampler *r);
 
 /* ---- state / introspection ----------------------------------------------- */
 void gar_reset(gar_resampler *r);                       /* Reset (constant.go:429-444, resampler.go:325-340) */
@@ -204,6 +212,10 @@ void gar_profile_enable(gar_resampler *r, int32_t on);
  * flush, 4 polyphase stage with live cubic coefficients, 5 QualityQuick cubic
  * stage) since its last read. */
 gar_status gar_profile_read(gar_resampler *r, int32_t kind, double *ms, int64_t *launches);
+/* Spread of the launches the last gar_profile_read of `kind` summed: min, median, max ms per launch
+ * (zeros when there were none). */
+gar_status gar_profile_launch_stats(gar_resampler *r, int32_t kind, double *min_ms, double *median_ms,
+                                    double *max_ms);
 /* Execution mode of pipeline stage `stage` of channel 0's group: *fused_plan = 1 when the
  * stage's DFT x2 + polyphase pair has a composite MFMA plan, *fused_now = 1 while the stream
  * still runs on it (0 after a stage-by-stage fallback: Process after Flush, the

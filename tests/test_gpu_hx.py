@@ -221,3 +221,28 @@ def test_hx_values_just_below_16(gar, O, cuda, chunks):
     if chunks is not None:
         one = run(gar, cuda, 44100, 48000, x, gar.QualityHigh, gar.F32)
         np.testing.assert_array_equal(got, one)
+
+
+def test_hxt_expired_wait_is_a_device_error(gar, cuda, monkeypatch):
+    """An expired progress wait of the streaming kernel (hxt_kernel) is an error, not output
+    (VERDICT r04 item 2): the development knob GAR_HXT_FAULT=1 makes the compute waves' load count
+    unreachable (and the poll bound short), the status word reaches the host, gar_synchronize and
+    the next call return GAR_ERR_DEVICE naming hxt_kernel, and Reset recovers the handle."""
+    torch = cuda
+    frames = 44100 * 20  # a streaming (non-small) launch: hxt_kernel, stereo frames
+    x = torch.from_numpy(signal(frames, 2, 44100, seed=7).astype(np.float32)).cuda()
+    r = gar.New(gar.Config(44100, 48000, 2, gar.QualityHigh, ComputeDtype=gar.F32))
+    ref = r.process_device(x).clone()
+    torch.cuda.synchronize()
+    r.Reset()
+    monkeypatch.setenv("GAR_HXT_FAULT", "1")
+    r.process_device(x)  # asynchronous: enqueued fine
+    with pytest.raises(gar.ErrDevice, match="hxt_kernel"):
+        r.synchronize()
+    monkeypatch.delenv("GAR_HXT_FAULT")
+    with pytest.raises(gar.ErrDevice):  # poisoned until Reset
+        r.process_device(x)
+    r.Reset()
+    again = r.process_device(x).clone()
+    r.synchronize()
+    assert torch.equal(again, ref)
