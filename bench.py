@@ -633,16 +633,25 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
     else:
         # f64: MFMA-bound (f64 matrix rate); useful flops of the dominant stage's own design
         flops_step = 2.0 * st_geom.useful_macs_per_output * st_out
+        if dom == 0 and not prof[2][1] and sidx > 0 and geoms[sidx - 1][1].kind == 3:
+            # pair launches (bg_pair_kernel): the decimator stage before the composite runs inside the
+            # same launch, so its useful flops belong to it too
+            flops_step += 2.0 * geoms[sidx - 1][1].useful_macs_per_output * st_in
         fl_launch = flops_step / per_step
         achieved = fl_launch / launch_s / 1e12 if launches else None
         roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
-        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel", "bg_rb_kernel"]
+        paired = dom == 0 and not prof[2][1] and sidx > 0 and geoms[sidx - 1][1].kind == 3
+        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel", "bg_rb_kernel", "bg_pair_kernel"]
         chunked = bool(w["chunk"])
-        kname = (f"{'poly_kernel<double>' if dom == 4 else ('bg_rb_kernel<double>' if chunked else 'bg_kernel<double>')} ({KIND_NAMES[dom]}, stage {sidx}: "
-                 f"{48000:g}->{48000 * st_ratio:g} Hz engine, v_mfma_f64_16x16x4_f64)")
-        algo_unit_bytes = (st_in + st_out) * 8 / per_step
+        kern = ('poly_kernel<double>' if dom == 4 else
+                ('bg_pair_kernel<double> (decimator items + ' if paired else '') +
+                ('bg_rb_kernel<double>' if chunked else 'bg_kernel<double>'))
+        kname = (f"{kern} ({KIND_NAMES[dom]}, stage {sidx}: {48000:g}->{48000 * st_ratio:g} Hz engine"
+                 f"{', with the decimator stage before it in the same launch)' if paired else ''}, v_mfma_f64_16x16x4_f64)")
+        # a pair launch reads the decimator's input (the stream) and writes the composite's output
+        algo_unit_bytes = ((frames * C if paired else st_in) + st_out) * 8 / per_step
         roof["useful_macs_per_output"] = round(st_geom.useful_macs_per_output, 2)
         roof["stage_outputs_per_step"] = int(st_out)
     roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[key]

@@ -494,14 +494,97 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
 // workgroups walking every row block.
 // History keep of a bg_rb_kernel launch (the `copy(history, history[consumed:])` of the stage):
 // element i of the new history is copied by thread i (mod the grid) of the flattened grid, issued right after the program's A / B loads so its memory round trip overlaps theirs.
+// Workgroup wg of nwg (the launch's grid, or the part of a pair launch running this stage).
 template <class TC>
-__device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g) {
+__device__ __forceinline__ void bgRbHistKeepW(const SrcDesc& src, const BgGrid& g, int wg, int nwg) {
     if (g.hn <= 0 || (g.dbg & 64)) return;
     const int64_t total = g.hn * g.C;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    for (int64_t i = static_cast<int64_t>(wg) * blockDim.x + threadIdx.x; i < total;
+         i += static_cast<int64_t>(nwg) * blockDim.x) {
         const int64_t t = i / g.C;
         static_cast<TC*>(g.hdst)[i] = srcRead<TC>(src, g.ht0 + t, static_cast<int>(i - t * g.C));
+    }
+}
+template <class TC>
+__device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g) {
+    bgRbHistKeepW<TC>(src, g, blockIdx.x, gridDim.x);
+}
+
+// One (column block, row block) item v of a bg_rb_kernel launch.  keep: this workgroup's share
+// (workgroup wg of nwg) of the history keep rides on this item.
+template <class TC, int NS>
+__device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
+                                         typename Acc<TC>::V (*slots)[64], bool keep, int wg, int nwg) {
+    typedef typename Acc<TC>::V V;
+    const int lane = threadIdx.x & 63;
+    const int wt = threadIdx.x >> 6;
+    const TC* Aimg = static_cast<const TC*>(p.A);
+    const int b = v / p.nrb, rb = v - b * p.nrb;
+    const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
+    const int col = b * 16 + (lane & 15);
+    const bool colOk = col < g.ncols;
+    const int c = colOk ? col % g.C : 0;
+    const int64_t a = g.a_lo + (colOk ? col / g.C : 0);  // G = 1
+    V r = {0, 0, 0, 0};
+    if (keep && wt >= np) bgRbHistKeepW<TC>(src, g, wg, nwg);  // waves that run no program
+    if (wt < np) {
+        const int pr = ps + wt;
+        const int k0 = g.rbK0[pr];
+        TC A[NS], B[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+        // rows of this lane: t0 + 4 s, s < NS (the zero-A tail steps read finite rows too)
+        const int64_t t0 = a * g.Qc + k0 + (lane >> 4);
+        const int64_t lo = a * g.Qc + k0, hi = lo + 4 * NS;
+        const TC* dp = nullptr;
+        int64_t ds = 0;
+        if (colOk && hi <= src.valid_end && lo >= 0 && !(g.dbg & (128 | 256))) {
+            if (srcSameType<TC>(src) && src.in && lo >= src.in_base && hi <= src.in_base + src.in_len) {
+                dp = static_cast<const TC*>(src.in) + (t0 - src.in_base) * src.in_fs + static_cast<int64_t>(c) * src.in_cs;
+                ds = 4 * src.in_fs;
+            } else if (src.hist && lo >= src.hist_base && hi <= src.hist_base + src.hist_len) {
+                dp = static_cast<const TC*>(src.hist) + (t0 - src.hist_base) * src.hist_ld + c;
+                ds = 4 * src.hist_ld;
+            }
+        }
+        if (g.dbg & 16) {  // development (GAR_BG_DBG): no B loads
+#pragma unroll
+            for (int s = 0; s < NS; ++s) B[s] = TC(s);
+        } else if (dp) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) B[s] = dp[s * ds];
+        } else if (srcSameType<TC>(src) && !(g.dbg & 256)) {
+            // window across the history seam / past the input: branch-free gathers, so the NS
+            // loads issue together (a branchy srcRead per step waits out each round trip)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) B[s] = srcReadBF<TC>(src, t0 + 4 * s, c, colOk, Aimg);
+        } else {
+#pragma unroll
+            for (int s = 0; s < NS; ++s) B[s] = colOk ? srcRead<TC>(src, t0 + 4 * s, c) : TC(0);
+        }
+        if (keep) bgRbHistKeepW<TC>(src, g, wg, nwg);  // its round trip beside A / B's
+        // every A / B load issued before the first MFMA: one memory round trip for the program
+        // (left alone, the scheduler interleaves load -> wait -> MFMA, NS round trips deep)
+        __builtin_amdgcn_sched_barrier(0);
+        V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+            else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+        }
+        r = acc0 + acc1;
+        if (np > 1) slots[wt][lane] = r;
+    }
+    if (np > 1) {
+        __syncthreads();
+        if (wt == 0) {
+            V sum = slots[0][lane];
+            for (int k = 1; k < np; ++k) sum += slots[k][lane];
+            if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+        }
+        __syncthreads();  // slots free for the next (column block, row block)
+    } else if (wt == 0 && !(g.dbg & 2)) {
+        storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
     }
 }
 
@@ -509,80 +592,10 @@ template <class TC, int NS>
 __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
     typedef typename Acc<TC>::V V;
     __shared__ V slots[kBgRbMaxWaves][64];
-    const int lane = threadIdx.x & 63;
-    const int wt = threadIdx.x >> 6;
-    const TC* Aimg = static_cast<const TC*>(p.A);
     const int nv = g.nblocks * p.nrb;
-    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
-        const int b = v / p.nrb, rb = v - b * p.nrb;
-        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
-        const int col = b * 16 + (lane & 15);
-        const bool colOk = col < g.ncols;
-        const int c = colOk ? col % g.C : 0;
-        const int64_t a = g.a_lo + (colOk ? col / g.C : 0);  // G = 1
-        V r = {0, 0, 0, 0};
-        if (wt < np) {
-            const int pr = ps + wt;
-            const int k0 = g.rbK0[pr];
-            TC A[NS], B[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
-            // rows of this lane: t0 + 4 s, s < NS (the zero-A tail steps read finite rows too)
-            const int64_t t0 = a * g.Qc + k0 + (lane >> 4);
-            const int64_t lo = a * g.Qc + k0, hi = lo + 4 * NS;
-            const TC* dp = nullptr;
-            int64_t ds = 0;
-            if (colOk && hi <= src.valid_end && lo >= 0 && !(g.dbg & (128 | 256))) {
-                if (srcSameType<TC>(src) && src.in && lo >= src.in_base && hi <= src.in_base + src.in_len) {
-                    dp = static_cast<const TC*>(src.in) + (t0 - src.in_base) * src.in_fs + static_cast<int64_t>(c) * src.in_cs;
-                    ds = 4 * src.in_fs;
-                } else if (src.hist && lo >= src.hist_base && hi <= src.hist_base + src.hist_len) {
-                    dp = static_cast<const TC*>(src.hist) + (t0 - src.hist_base) * src.hist_ld + c;
-                    ds = 4 * src.hist_ld;
-                }
-            }
-            if (g.dbg & 16) {  // development (GAR_BG_DBG): no B loads
-#pragma unroll
-                for (int s = 0; s < NS; ++s) B[s] = TC(s);
-            } else if (dp) {
-#pragma unroll
-                for (int s = 0; s < NS; ++s) B[s] = dp[s * ds];
-            } else if (srcSameType<TC>(src) && !(g.dbg & 256)) {
-                // window across the history seam / past the input: branch-free gathers, so the NS
-                // loads issue together (a branchy srcRead per step waits out each round trip)
-#pragma unroll
-                for (int s = 0; s < NS; ++s) B[s] = srcReadBF<TC>(src, t0 + 4 * s, c, colOk, Aimg);
-            } else {
-#pragma unroll
-                for (int s = 0; s < NS; ++s) B[s] = colOk ? srcRead<TC>(src, t0 + 4 * s, c) : TC(0);
-            }
-            if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside A / B's
-            // every A / B load issued before the first MFMA: one memory round trip for the program
-            // (left alone, the scheduler interleaves load -> wait -> MFMA, NS round trips deep)
-            __builtin_amdgcn_sched_barrier(0);
-            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
-                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
-            }
-            r = acc0 + acc1;
-            if (np > 1) slots[wt][lane] = r;
-        }
-        if (np > 1) {
-            __syncthreads();
-            if (wt == 0) {
-                V sum = slots[0][lane];
-                for (int k = 1; k < np; ++k) sum += slots[k][lane];
-                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
-            }
-            __syncthreads();  // slots free for the next (column block, row block)
-        } else if (wt == 0 && !(g.dbg & 2)) {
-            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
-        }
-    }
-    const int rb0 = static_cast<int>(blockIdx.x) % p.nrb;  // the first (column block, row block) of this workgroup
-    if (wt >= g.rbStart[rb0 + 1] - g.rbStart[rb0]) bgRbHistKeep<TC>(src, g);  // waves that ran no program
+    for (int v = blockIdx.x; v < nv; v += gridDim.x)  // uniform per workgroup
+        bgRbItem<TC, NS>(p, src, od, g, v, slots, v == static_cast<int>(blockIdx.x), blockIdx.x, gridDim.x);
+    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);  // a workgroup without an item
 }
 
 // Small launches of row-block-aligned plans, time-major (default; bg_rb_kernel is the GAR_BG_RT=0
@@ -600,10 +613,11 @@ inline size_t bgRtLds(int Qc, int Kread, int nprog, size_t esz) {
     return (win + 15) / 16 * 16 + static_cast<size_t>(nprog) * 64 * 4 * esz;
 }
 
+// One (row block, channel, chunk block) item v of a bg_rt_kernel launch (smem: the window + slots).
 template <class TC, int NS>
-__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+__device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
+                                         unsigned char* smem, bool keep, int wg, int nwg) {
     typedef typename Acc<TC>::V V;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
     const TC* Aimg = static_cast<const TC*>(p.A);
@@ -613,75 +627,81 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
     TC* win = reinterpret_cast<TC*>(smem);
     V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(nphys) * sizeof(TC) + 15) / 16 * 16);
     const int nkb = (g.nchunk + 15) / 16;
-    const int nv = p.nrb * g.C * nkb;
     const bool same = srcSameType<TC>(src);
-    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
-        const int rb = v % p.nrb, cb = v / p.nrb;
-        const int c = cb / nkb, kb = cb - c * nkb;
-        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
-        TC A[NS];
-        int k0 = 0;
-        if (wt < np) {  // A lands while the window is staged
-            const int pr = ps + wt;
-            k0 = g.rbK0[pr];
+    const int rb = v % p.nrb, cb = v / p.nrb;
+    const int c = cb / nkb, kb = cb - c * nkb;
+    const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
+    TC A[NS];
+    int k0 = 0;
+    if (wt < np) {  // A lands while the window is staged
+        const int pr = ps + wt;
+        k0 = g.rbK0[pr];
 #pragma unroll
-            for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
-        }
-        // stage rows [0, nrow) of channel c from T: batches of kRtB loads per thread in flight
-        const int64_t T = (g.a_lo + 16 * static_cast<int64_t>(kb)) * Qc;
-        constexpr int kRtB = 8;  // loads per thread in flight: the decimator's ~1.7k-row window in one round trip
-        for (int r0 = threadIdx.x; r0 < nrow; r0 += kRtB * blockDim.x) {
-            TC vv[kRtB];
-#pragma unroll
-            for (int u = 0; u < kRtB; ++u) {
-                const int r = r0 + u * blockDim.x;
-                vv[u] = (g.dbg & 16) ? TC(r) : (same ? srcReadBF<TC>(src, T + r, c, r < nrow, Aimg) : (r < nrow ? srcRead<TC>(src, T + r, c) : TC(0)));
-            }
-#pragma unroll
-            for (int u = 0; u < kRtB; ++u) {
-                const int r = r0 + u * blockDim.x;
-                if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
-            }
-        }
-        if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside the staging
-        __syncthreads();  // window staged
-        const int n = lane & 15, kq = lane >> 4;
-        const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
-        const bool colOk = 16 * kb + n < g.nchunk;
-        V r = {0, 0, 0, 0};
-        if (wt < np) {
-            // row n*Qc + k0 + 4s + kq -> LDS index n*(Qc+pad) + x + pad*(x / Qc), x = k0 + 4s + kq
-            const int x0 = k0 + kq;
-            int q = x0 / Qc, rem = x0 - q * Qc;
-            const int nb = n * (Qc + pad);
-            TC B[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                B[s] = win[nb + q * (Qc + pad) + rem];
-                rem += 4;
-                if (rem >= Qc) { rem -= Qc; ++q; }
-            }
-            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
-                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
-            }
-            r = acc0 + acc1;
-            if (np > 1) slots[wt * 64 + lane] = r;
-        }
-        if (np > 1) {
-            __syncthreads();
-            if (wt == 0) {
-                V sum = slots[lane];
-                for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
-                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
-            }
-        } else if (wt == 0 && !(g.dbg & 2)) {
-            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
-        }
-        __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
+        for (int s = 0; s < NS; ++s) A[s] = (g.dbg & 32) ? TC(s) : Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
     }
+    // stage rows [0, nrow) of channel c from T: batches of kRtB loads per thread in flight
+    const int64_t T = (g.a_lo + 16 * static_cast<int64_t>(kb)) * Qc;
+    constexpr int kRtB = 8;  // loads per thread in flight: the decimator's ~1.7k-row window in one round trip
+    for (int r0 = threadIdx.x; r0 < nrow; r0 += kRtB * blockDim.x) {
+        TC vv[kRtB];
+#pragma unroll
+        for (int u = 0; u < kRtB; ++u) {
+            const int r = r0 + u * blockDim.x;
+            vv[u] = (g.dbg & 16) ? TC(r) : (same ? srcReadBF<TC>(src, T + r, c, r < nrow, Aimg) : (r < nrow ? srcRead<TC>(src, T + r, c) : TC(0)));
+        }
+#pragma unroll
+        for (int u = 0; u < kRtB; ++u) {
+            const int r = r0 + u * blockDim.x;
+            if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
+        }
+    }
+    if (keep) bgRbHistKeepW<TC>(src, g, wg, nwg);  // its round trip beside the staging
+    __syncthreads();  // window staged
+    const int n = lane & 15, kq = lane >> 4;
+    const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
+    const bool colOk = 16 * kb + n < g.nchunk;
+    V r = {0, 0, 0, 0};
+    if (wt < np) {
+        // row n*Qc + k0 + 4s + kq -> LDS index n*(Qc+pad) + x + pad*(x / Qc), x = k0 + 4s + kq
+        const int x0 = k0 + kq;
+        int q = x0 / Qc, rem = x0 - q * Qc;
+        const int nb = n * (Qc + pad);
+        TC B[NS];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            B[s] = win[nb + q * (Qc + pad) + rem];
+            rem += 4;
+            if (rem >= Qc) { rem -= Qc; ++q; }
+        }
+        V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+            else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+        }
+        r = acc0 + acc1;
+        if (np > 1) slots[wt * 64 + lane] = r;
+    }
+    if (np > 1) {
+        __syncthreads();
+        if (wt == 0) {
+            V sum = slots[lane];
+            for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
+            if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+        }
+    } else if (wt == 0 && !(g.dbg & 2)) {
+        storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+    }
+    __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
+}
+
+template <class TC, int NS>
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int nkb = (g.nchunk + 15) / 16;
+    const int nv = p.nrb * g.C * nkb;
+    for (int v = blockIdx.x; v < nv; v += gridDim.x)  // uniform per workgroup
+        bgRtItem<TC, NS>(p, src, od, g, v, smem, v == static_cast<int>(blockIdx.x), blockIdx.x, gridDim.x);
     // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
     // no second pass); a workgroup without one copies it here
     if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
@@ -788,6 +808,58 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rc_kernel(BgDev p, SrcD
     // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
     // no second pass); a workgroup without one copies it here
     if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
+}
+
+// ---- pair launch: a decimator stage and the next stage's composite FIR in ONE launch --------------
+// A streaming call of a multi-stage f64 pipeline (cfg5: decimator 96k -> 48k, then the DFT x2 +
+// polyphase composite 48k -> 44.1k, constant.go:308-337) was two dependent small launches; the
+// second waited out the first launch's tail and its own ramp (r04: 18.8 us per call for the
+// skeleton alone).  Here workgroups take tickets from a device counter: tickets [0, n0) are the
+// decimator's bg_rt items, [n0, n0 + n1) the composite's bg_rb items.  A ticket is only handed out
+// once every lower one has been, so every decimator item is running or done when a composite item
+// starts: no dispatch-order or co-residency assumption.  A composite item first waits until all n0
+// decimator items have published (agent-scope release / acquire through the second counter: the
+// decimated samples cross XCDs through L2 write-back), then runs exactly bg_rb_kernel's item --
+// the same programs, the same sums, the same bits.  Both counters only grow (unsigned wrap, signed
+// differences); the host keeps their values at launch (tick0, done0).
+struct BgPair {
+    BgDev p0, p1;
+    SrcDesc s0, s1;
+    OutDesc o0, o1;
+    BgGrid g0, g1;
+    unsigned* ctr;           // [0] tickets handed out, [1] decimator items published
+    unsigned tick0, done0;   // their values when this launch starts
+    int n0, n1;              // items of each stage
+    int* err;                // device status word: the hand-off wait expired (code kBgErrPairWait)
+};
+
+template <int NS0, int NS1>
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_pair_kernel(BgPair a) {
+    typedef typename Acc<double>::V V;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ V slots[kBgRbMaxWaves][64];
+    __shared__ int tk;
+    if (threadIdx.x == 0) tk = static_cast<int>(__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.tick0);
+    __syncthreads();
+    const int t = tk;
+    if (t < a.n0) {
+        bgRtItem<double, NS0>(a.p0, a.s0, a.o0, a.g0, t, smem, true, t, a.n0);
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed in L2
+        __syncthreads();                // ... and every other wave's
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (t < a.n0 + a.n1) {
+        if (threadIdx.x == 0) {
+            const unsigned want = a.done0 + static_cast<unsigned>(a.n0);
+            int it = 0;
+            for (; it < (1 << 22); ++it) {
+                if (static_cast<int>(__hip_atomic_load(a.ctr + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (it >= (1 << 22) && a.err) __hip_atomic_store(a.err, kBgErrPairWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        bgRbItem<double, NS1>(a.p1, a.s1, a.o1, a.g1, t - a.n0, slots, true, t - a.n0, a.n1);
+    }
 }
 
 template <class TC, int NS>

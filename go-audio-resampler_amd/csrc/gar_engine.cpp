@@ -634,6 +634,7 @@ struct gar_resampler {
     // (hxt_kernel: an expired progress wait) writes a nonzero code; every ABI call checks it first
     int* errHost = nullptr;
     int* errDev = nullptr;
+    gar::BgPairCtr pairCtr;  // device counters of decimator + composite pair launches
     gar_config cfg{};
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
@@ -665,17 +666,40 @@ void trimHost(Handle* h) {
     if (h->hostOut.cap > kPinKeep) h->hostOut.release();
 }
 
+// A decimator launch held back so that the next stage's composite launch can take it along
+// (launchBgPair: one launch per streaming call of a decimator -> DFT x2 + polyphase pipeline).
+struct PendingBg {
+    bool on = false;
+    const BgDev* p = nullptr;
+    SrcDesc src{};
+    OutDesc od{};
+    int C = 0;
+    HistCopy hc;
+};
+
 struct Ctx {
     Handle* h;
     Group* g;
     hipStream_t s;
     bool launch;
+    PendingBg* pend = nullptr;  // set for real launches (not the counting passes)
+    bool deferNext = false;     // the next decimator launch may wait for its partner
 };
 
-// launchBg bracketed by HIP events on the launch stream when profiling is on.
+template <class L>
+hipError_t timedRaw(Ctx& x, int tag, L&& launch);
+void flushPending(Ctx& x);
+
 // A launch bracketed by HIP events on its stream when profiling is on (tag = gar_profile_read kind).
+// Any held-back decimator launch goes first (stream order = the stages' order).
 template <class L>
 hipError_t timed(Ctx& x, int tag, L&& launch) {
+    flushPending(x);
+    return timedRaw(x, tag, launch);
+}
+
+template <class L>
+hipError_t timedRaw(Ctx& x, int tag, L&& launch) {
     if (!x.h->profile) return launch();
     hipEvent_t a, b;
     if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
@@ -693,8 +717,46 @@ hipError_t timed(Ctx& x, int tag, L&& launch) {
     return e;
 }
 
+// Launches a held-back decimator on its own (its partner did not come, or cannot pair).
+void flushPending(Ctx& x) {
+    if (!x.pend || !x.pend->on) return;
+    PendingBg& d = *x.pend;
+    d.on = false;
+    HistCopy hc = d.hc;
+    hc.done = false;
+    HIPCHK(timedRaw(x, 2, [&] { return launchBg(*d.p, d.src, d.od, d.C, x.s, &hc); }));
+    // the keep was promised to the stage's bookkeeping when the launch was held back
+    if (hc.n > 0 && hc.dst && !hc.done)
+        HIPCHK(launchGather(1, d.src, hc.dst, hc.t0, hc.n, d.C, x.s));
+}
+
 hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C,
                    HistCopy* hc = nullptr) {
+    if (x.deferNext && x.pend && tag == 2 && p.f64 && !x.pend->on) {  // hold the decimator back for its partner
+        x.deferNext = false;
+        PendingBg& d = *x.pend;
+        d.on = true;
+        d.p = &p;
+        d.src = src;
+        d.od = od;
+        d.C = C;
+        d.hc = hc ? *hc : HistCopy();
+        if (hc && hc->n > 0 && hc->dst) hc->done = true;  // taken by the pair launch or by flushPending
+        return hipSuccess;
+    }
+    if (x.pend && x.pend->on && tag == 0 && p.f64) {  // the composite of the same call: one launch for both
+        PendingBg& d = *x.pend;
+        HistCopy h0 = d.hc;
+        h0.done = false;
+        const hipError_t e = timedRaw(x, 0, [&] {
+            return launchBgPair(*d.p, d.src, d.od, &h0, p, src, od, hc, C, x.s, x.h->pairCtr);
+        });
+        if (e != hipErrorNotSupported) {
+            d.on = false;
+            if (e == hipSuccess && h0.n > 0 && h0.dst && !h0.done) throw DevError{hipErrorUnknown, "pair launch left the decimator's history keep"};
+            return e;
+        }
+    }
     return timed(x, tag, [&] { return launchBg(p, src, od, C, x.s, hc); });
 }
 
@@ -738,6 +800,7 @@ void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
     if (!x.launch) { hs.base = k0; hs.len = k1 - k0; hs.zero = false; return; }
     const int other = 1 - hs.cur;
     hs.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(k1 - k0, 1)) * C * tc);
+    flushPending(x);
     HIPCHK(launchGather(x.h->f64, src, hs.buf[other].p, k0, k1 - k0, C, x.s));
     hs.cur = other;
     hs.base = k0;
@@ -828,8 +891,10 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
             return nout;
         }
         case EngineKind::Passthrough: {
-            if (x.launch && !in.zeros)
+            if (x.launch && !in.zeros) {
+                flushPending(x);
                 HIPCHK(launchCopy(in.p, in.f64, in.fs, in.cs, out.p, out.f64, out.fs, out.cs, n, C, x.s));
+            }
             c.y_count += n;
             return n;
         }
@@ -1015,12 +1080,22 @@ int64_t chainProcess(Ctx& x, const InView& in, const OutView& out, std::vector<i
             }
         }
         int64_t m = 0;
+        // decimator -> fused DFT x2 + polyphase (f64): the two launches of this call go out as one
+        // (launchBgPair); knob GAR_BG_PAIR=0 keeps them apart
+        static const bool pairOn = !(std::getenv("GAR_BG_PAIR") && std::getenv("GAR_BG_PAIR")[0] == '0');
+        x.deferNext = pairOn && x.launch && x.pend && !last && x.h->f64 && x.h->stages[i]->d.kind == EngineKind::Decim &&
+                      x.h->stages[i + 1]->d.kind == EngineKind::DftPoly && x.h->stages[i + 1]->fused &&
+                      !x.g->cnt[i + 1].staged;
+        const bool held = x.pend && x.pend->on;  // stage i - 1's decimator waits for this stage
         if (cur.n >= 1) m = stageProcess(x, i, cur, o);  // Available() >= GetMinInput() (constant.go:277,314)
+        x.deferNext = false;
+        if (held && x.pend->on) flushPending(x);  // this stage launched nothing to pair with
         sizes[i] = m;
         InView nx;
         nx.p = o.p; nx.fs = o.fs; nx.cs = o.cs; nx.f64 = o.f64; nx.n = m;
         cur = nx;
     }
+    flushPending(x);
     return cur.n;
 }
 
@@ -1156,7 +1231,8 @@ int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool
         return n;
     }
     h->scratchSizes = sizes;
-    Ctx x{h, &g, s, true};
+    PendingBg pend;
+    Ctx x{h, &g, s, true, &pend};
     std::vector<int64_t> s2;
     const int64_t got = flush ? chainFlush(x, out, s2) : chainProcess(x, in, out, s2);
     if (got != n) { st = GAR_ERR_INTERNAL; g_err = "size mismatch between count and launch"; }
@@ -1216,10 +1292,12 @@ bool devFault(Handle* h) {
     const int v = __atomic_load_n(h->errHost, __ATOMIC_ACQUIRE);
     if (!v) return false;
     h->poisoned = true;
-    g_err = std::string("device error reported by hxt_kernel: ") +
-            (v == kHxtErrLoadWait ? "a compute wave's LDS load-progress wait expired"
-                                  : (v == kHxtErrSlotWait ? "a loader's LDS ring-slot wait expired" : "unknown code")) +
-            " (code " + std::to_string(v) + "); outputs of the launch are invalid; call Reset";
+    const char* what = v == kHxtErrLoadWait   ? "hxt_kernel: a compute wave's LDS load-progress wait expired"
+                       : v == kHxtErrSlotWait ? "hxt_kernel: a loader's LDS ring-slot wait expired"
+                       : v == kBgErrPairWait  ? "bg_pair_kernel: a composite item's wait for the decimator items expired"
+                                              : "unknown code";
+    g_err = std::string("device error reported by ") + what + " (code " + std::to_string(v) +
+            "); outputs of the launch are invalid; call Reset";
     return true;
 }
 
@@ -1322,6 +1400,10 @@ gar_status initDevice(Handle* h) {
     void* d = nullptr;
     HIPCHK(hipHostGetDevicePointer(&d, w, 0));
     h->errDev = static_cast<int*>(d);
+    void* pc = nullptr;
+    HIPCHK(hipMalloc(&pc, 2 * sizeof(unsigned)));
+    HIPCHK(hipMemset(pc, 0, 2 * sizeof(unsigned)));
+    h->pairCtr.dev = static_cast<unsigned*>(pc);
     return GAR_OK;
 }
 
@@ -1583,6 +1665,7 @@ void gar_free(gar_resampler* r) {
         r->groups.clear();
         r->stages.clear();
         if (r->failEv) (void)hipEventDestroy(r->failEv);
+        if (r->pairCtr.dev) (void)hipFree(r->pairCtr.dev);
         if (r->errHost) (void)hipHostFree(r->errHost);
         if (r->stream) (void)hipStreamDestroy(r->stream);
     } catch (...) {
@@ -1895,6 +1978,7 @@ void gar_reset(gar_resampler* r) {
             if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
             (void)hipGetLastError();
             if (r->errHost) __atomic_store_n(r->errHost, 0, __ATOMIC_RELEASE);  // every launch that could write it has drained
+            if (r->pairCtr.dev && hipMemset(r->pairCtr.dev, 0, 2 * sizeof(unsigned)) == hipSuccess) r->pairCtr.tick = r->pairCtr.done = 0;
             r->groups.clear();
             r->groups.push_back(freshGroup(r, 0, r->channels));
             r->poisoned = false;

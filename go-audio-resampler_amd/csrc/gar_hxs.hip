@@ -48,6 +48,8 @@ unsigned long long* profBuf() {
                     if (h[34]) fprintf(stderr, "hxt roles per block (cycles): compute wave 0 %.0f (waiting %.0f), loader 0 %.0f (waiting %.0f), n %llu\n",
                                        static_cast<double>(h[30]) / h[34], static_cast<double>(h[32]) / h[34], static_cast<double>(h[31]) / h[34],
                                        static_cast<double>(h[33]) / h[34], h[34]);
+                    if (h[34]) fprintf(stderr, "hxt compute wave 0: entry -> first group %.0f cycles, last group -> exit %.0f cycles\n",
+                                       static_cast<double>(h[35]) / h[34], static_cast<double>(h[36]) / h[34]);
                     if (h[44]) fprintf(stderr, "hxq wave 0 (cycles): entry->barrier 1 %.0f, ->image %.0f, ->MFMA+stores issued %.0f, ->drained %.0f, n %llu\n",
                                        static_cast<double>(h[40]) / h[44], static_cast<double>(h[41]) / h[44], static_cast<double>(h[42]) / h[44],
                                        static_cast<double>(h[43]) / h[44], h[44]);

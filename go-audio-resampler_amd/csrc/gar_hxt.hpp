@@ -304,10 +304,16 @@ __device__ __forceinline__ void hxtArrive(lds_i32* arr, lds_i32* done, int j, in
 
 // *done >= need, bounded; on expiry the abort word and the handle's status word are set.
 __device__ __forceinline__ void hxtWait(const HxsArgs& x, const HxtSync& sy, const lds_i32* done, int need, int code,
-                                        int lane) {
+                                        int lane, unsigned long long* waited = nullptr) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (*reinterpret_cast<const volatile lds_i32*>(done) >= need) return;  // the common case: one read
     if (*reinterpret_cast<const volatile lds_i32*>(sy.abort)) return;      // after an expiry: no more waiting
+    const unsigned long long t0 = (kHxsDev && waited) ? __builtin_amdgcn_s_memtime() : 0;
+    struct Acc {  // development (GAR_HXS_PROF): cycles spent in this wait
+        unsigned long long* w;
+        unsigned long long t0;
+        __device__ ~Acc() { if (kHxsDev && w) *w += __builtin_amdgcn_s_memtime() - t0; }
+    } acc{kHxsDev ? waited : nullptr, t0};
     const int pmax = x.pollMax;
     int it = 0;
     for (; it < pmax; ++it) {
@@ -338,7 +344,7 @@ __device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
 // registers just freed.
 template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
-                                           int lane) {
+                                           int lane, unsigned long long* waited) {
     const HxsArgsP xp = hxsCold();
     const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
     const int P = (Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
@@ -373,7 +379,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (j >= P) {
                     if (j == P) p0 = Wg;  // Wg < R
                     need = last < 0 ? 0 : need + 1;
-                    if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpDone, need, kHxtErrSlotWait, lane);  // development 64: loaders never wait
+                    if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpDone, need, kHxtErrSlotWait, lane, waited);  // development 64: loaders never wait
                     last += GQ;
                 }
                 if (!((dbg & 16) && j >= P)) {
@@ -398,7 +404,8 @@ template <int NS, int VST, bool FAST>
 __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int wt, int lane,
                                           const h8v (&Ah)[NS], const h8v (&Al)[NS], uint32_t laneOff, int u0, int P,
                                           int nslot, const HxtRole& ro, char* obase, int64_t pstride, int64_t aCol,
-                                          int64_t oRow0, bool colOk, int ccol, bool fullRb) {
+                                          int64_t oRow0, bool colOk, int ccol, bool fullRb, unsigned long long* st) {
+    // st (development, GAR_HXS_PROF): [0] cycles waiting for loads, [1] first group's start, [2] last group's end
     const int sh = -(x.ea + kHxXs);
     const int GQ = x.G * x.Qc;
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
@@ -433,7 +440,8 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         while (first < p0) first += ro.st;
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
-            if (!(dbg & 32)) hxtWait(x, sy, sy.ldDone, P + g + x.faultNeed, kHxtErrLoadWait, lane);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
+            if (!(dbg & 32)) hxtWait(x, sy, sy.ldDone, P + g + x.faultNeed, kHxtErrLoadWait, lane, st);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
+            if (kHxsDev && st && st[1] == 0) st[1] = __builtin_amdgcn_s_memtime();
             // the lane's ring offset, recomputed per group (a value held across the group loop spills,
             // and its reload's vmcnt(0) would wait for this wave's output stores)
             int ln = lane;
@@ -472,11 +480,12 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         }
         hxtArrive(sy.cpArr, sy.cpDone, g, x.ncomp, lane);  // this wave's reads of group g's window are done
     }
+    if (kHxsDev && st) st[2] = __builtin_amdgcn_s_memtime();
 }
 
 template <int NS, int VST>
 __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int b, int wt,
-                                           int lane) {
+                                           int lane, unsigned long long* st) {
     // A of the wave's row block (kept in registers only inside this role: the loaders' registers
     // are the load buffers)
     const HxtRole ro = hxtRole(x, wt);
@@ -507,10 +516,10 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
                   (VST == 2 ? 0 : ccol * x.out_cs);
     if (__builtin_amdgcn_ballot_w64(!laneFast) == 0)
         hxtGroups<NS, VST, true>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                 colOk, ccol, fullRb);
+                                 colOk, ccol, fullRb, st);
     else
         hxtGroups<NS, VST, false>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                  colOk, ccol, fullRb);
+                                  colOk, ccol, fullRb, st);
 }
 
 // FMT: 1 stereo f32 frames, 2 rows of 16 f32 channels.  VST: 0 any f32 layout, 1 channel-contiguous
@@ -536,6 +545,12 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     const int wt = uni(threadIdx.x >> 6);
     const bool comp = wt < x.ncomp;
     if (threadIdx.x == 0) *sy.abort = 0;  // sticky for the launch (ordered by the first block's barriers)
+    // development (GAR_HXS_PROF): wave 0 (compute) and the first loader stamp their first block
+    const bool stampW = kHxsDev && x.prof && lane == 0 && (wt == 0 || wt == x.ncomp);
+    const unsigned long long tEntry = stampW ? __builtin_amdgcn_s_memtime() : 0;
+    const unsigned long long rEntry = stampW ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long st[3] = {0, 0, 0};
+    unsigned long long tBlockEnd = 0;
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
         __syncthreads();  // the previous block's ring reads and fixup done
@@ -546,8 +561,11 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
         if (threadIdx.x < 2 * kHxtSlots + 2) sy.ldArr[threadIdx.x] = 0;  // arrivals, ldDone, cpDone
         if (threadIdx.x == 64) *s.flag = 0;
         __syncthreads();
-        if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane);
-        else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane);
+        const bool first = bi == static_cast<int>(blockIdx.x);
+        unsigned long long* stp = (stampW && first) ? st : nullptr;
+        if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane, stp);
+        else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane, stp);
+        if (stampW && first) tBlockEnd = __builtin_amdgcn_s_memtime();
         __syncthreads();  // every wave's part of the block done; flag final
         if (*s.flag) {  // uniform
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
@@ -557,6 +575,23 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     }
     if (x.hn > 0) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
                               static_cast<int64_t>(gridDim.x) * blockDim.x);
+    if (stampW) {  // development: role cycles of the first block, fill / drain, workgroup life, launch span
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tExit = __builtin_amdgcn_s_memtime(), rExit = __builtin_amdgcn_s_memrealtime();
+        if (wt == 0) {
+            atomicAdd(x.prof + 30, tBlockEnd - tEntry);
+            atomicAdd(x.prof + 32, st[0]);
+            atomicAdd(x.prof + 34, 1ull);
+            atomicAdd(x.prof + 35, st[1] ? st[1] - tEntry : 0ull);  // entry -> first group runs (fill)
+            atomicAdd(x.prof + 36, tExit - (st[2] ? st[2] : tExit));  // last group done -> exit (drain)
+            atomicMin(x.prof + 10, rEntry);
+            atomicMax(x.prof + 11, rExit);
+            if (blockIdx.x < 4096) { x.prof[64 + 2 * blockIdx.x] = rEntry; x.prof[65 + 2 * blockIdx.x] = rExit - rEntry; }
+        } else {
+            atomicAdd(x.prof + 31, tBlockEnd - tEntry);
+            atomicAdd(x.prof + 33, st[0]);
+        }
+    }
 }
 
 template <int NS, int FMT, int VST, int NL>

@@ -67,12 +67,138 @@ hipError_t bgLaunchF32a(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int threads,
                         size_t lds, int64_t blocks, hipStream_t st, bool globalB);
 
+// Small-launch geometry of a row-block-aligned f64 plan (stream chunks): returns the launch mode
+// (0 not a small launch; 1 bg_rb_kernel, 2 bg_rt_kernel, 3 bg_rc_kernel) with g, the dynamic LDS and
+// the grid filled in.  The history keep hc is taken (hc->done) when the mode is not 0.
+static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, int ncu, BgGrid& g, size_t& lds,
+                       int64_t& blocks) {
+    static const int knobDbg = std::getenv("GAR_BG_DBG") ? std::atoi(std::getenv("GAR_BG_DBG")) : 0;
+    const int64_t a_lo = od.o_lo / p.Pc;
+    const int64_t a_hi = (od.o_hi + p.Pc - 1) / p.Pc;
+    const int64_t nmac = a_hi - a_lo;
+    // small launch of a row-block-aligned f64 plan (stream chunks): one (column block, row block) per
+    // workgroup, one macro period per column (bg_rb_kernel) -- same programs, same sums
+    if (!(p.f64 && p.rbAligned && p.rbStart && p.hRbStart && p.nrb <= kBgRbKMaxRb && p.nprog <= kBgRbKMaxProg &&
+          (nmac * C + 15) / 16 <= 2 * static_cast<int64_t>(ncu) && !(knobDbg & 8)))
+        return 0;
+    g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;
+    g.nprog = p.nprog;
+    g.kch = p.kch;
+    g.nwt = p.nw;
+    g.ncg = p.ncg;
+    g.nred = p.nred;
+    g.nslots = p.nslots;
+    g.a_lo = a_lo;
+    g.rbMode = 1;
+    for (int i = 0; i <= p.nrb; ++i) g.rbStart[i] = p.hRbStart[i];
+    for (int i = 0; i < p.nprog; ++i) g.rbK0[i] = p.hRbK0[i];
+    g.G = 1;
+    g.W = p.Kc;
+    g.Wl = p.Kread;
+    g.Ws = g.Wl;
+    g.nchunk = static_cast<int>(nmac);
+    g.ncols = static_cast<int>(nmac * C);
+    g.nblocks = (g.ncols + 15) / 16;
+    g.dbg = knobDbg;
+    g.vst = 0;
+    g.parity = 0;
+    g.hdst = nullptr;
+    g.ht0 = g.hn = 0;
+    if (hc && hc->n > 0 && hc->dst) {
+        g.hdst = hc->dst;
+        g.ht0 = hc->t0;
+        g.hn = hc->n;
+        hc->done = true;
+    }
+    // time-major (bg_rt_kernel, knob GAR_BG_RT=0: bg_rb_kernel): workgroups = row blocks x channels
+    // x blocks of 16 consecutive macro periods, each window staged once in LDS
+    // Default: time-major for plans of one or two row blocks (the integer decimator: each window is
+    // staged once; 4800-frame cfg5 calls 26.8 -> 18.9 us), bg_rb_kernel otherwise (a plan of ten row
+    // blocks would stage every window ten times: the cfg5 composite 21.8 -> 33.6 us).
+    static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : -1;
+    const size_t rtLds = bgRtLds(p.Qc, p.Kread, p.maxPrb, 8);
+    if ((knobRt == 1 || (knobRt < 0 && p.nrb <= 2)) && rtLds <= 64 * 1024) {
+        g.rbMode = 2;
+        const int64_t nkb = (nmac + 15) / 16;
+        blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);
+        lds = rtLds;
+        return 2;
+    }
+    const size_t rcLds = bgRcLds(C, p.Qc, p.Kread, p.maxPrb, 8);
+    if (knobRt == 2 && rcLds <= 160 * 1024 - 1024) {
+        g.rbMode = 3;
+        blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
+        lds = rcLds;
+        return 3;
+    }
+    blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
+    lds = 0;
+    return 1;
+}
+
+static int numCUs() {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    return ncu;
+}
+
+// bg_pair_kernel instantiations (gar_bg_pair_*.hip): NS of the decimator's and the composite's programs
+hipError_t bgPairDispatch1(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
+hipError_t bgPairDispatch2(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
+hipError_t bgPairDispatch3(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
+static hipError_t bgPairDispatch(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st) {
+    if (NS0 <= 16) return bgPairDispatch1(NS0, NS1, a, lds, blocks, threads, st);
+    if (NS0 <= 28) return bgPairDispatch2(NS0, NS1, a, lds, blocks, threads, st);
+    return bgPairDispatch3(NS0, NS1, a, lds, blocks, threads, st);
+}
+
+hipError_t launchBgPair(const BgDev& p0, const SrcDesc& s0, const OutDesc& o0, HistCopy* h0, const BgDev& p1,
+                        const SrcDesc& s1, const OutDesc& o1, HistCopy* h1, int C, hipStream_t stream, BgPairCtr& ctr) {
+    if (!ctr.dev || !p0.f64 || !p1.f64 || o0.o_hi <= o0.o_lo || o1.o_hi <= o1.o_lo) return hipErrorNotSupported;
+    const int ncu = numCUs();
+    BgPair a{};
+    HistCopy t0 = h0 ? *h0 : HistCopy(), t1 = h1 ? *h1 : HistCopy();
+    t0.done = t1.done = false;
+    size_t lds0 = 0, lds1 = 0;
+    int64_t b0 = 0, b1 = 0;
+    if (bgSmallGrid(p0, o0, C, &t0, ncu, a.g0, lds0, b0) != 2) return hipErrorNotSupported;  // decimator: bg_rt items
+    if (bgSmallGrid(p1, o1, C, &t1, ncu, a.g1, lds1, b1) != 1) return hipErrorNotSupported;  // composite: bg_rb items
+    const int64_t n0 = (a.g0.nchunk + 15) / 16 * static_cast<int64_t>(C) * p0.nrb;
+    const int64_t n1 = static_cast<int64_t>(a.g1.nblocks) * p1.nrb;
+    if (n0 != b0 || n1 != b1 || n0 + n1 > 65535) return hipErrorNotSupported;  // one item per workgroup
+    a.p0 = p0; a.p1 = p1;
+    a.s0 = s0; a.s1 = s1;
+    a.o0 = o0; a.o1 = o1;
+    a.ctr = ctr.dev;
+    a.tick0 = ctr.tick;
+    a.done0 = ctr.done;
+    a.n0 = static_cast<int>(n0);
+    a.n1 = static_cast<int>(n1);
+    a.err = o1.err;
+    const int threads = 64 * std::max(p0.maxPrb, p1.maxPrb);
+    const hipError_t e = bgPairDispatch(p0.NS, p1.NS, a, lds0, n0 + n1, threads, stream);
+    if (e == hipSuccess) {
+        ctr.tick += static_cast<unsigned>(n0 + n1);
+        ctr.done += static_cast<unsigned>(n0);
+        if (h0) h0->done = t0.done;
+        if (h1) h1->done = t1.done;
+    }
+    return e;
+}
+
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
     if (od.o_hi <= od.o_lo) return hipSuccess;
     // f32 compute on the split-f16 kernel (every output of the launch, any input dtype)
     if (p.hx && !p.f64) return launchHx(*p.hx, src, od, C, stream, hc);
     const int sz = p.f64 ? 8 : 4;
     BgGrid g;
+    const int ncu = numCUs();
+    {
+        size_t lds = 0;
+        int64_t blocks = 0;
+        if (bgSmallGrid(p, od, C, hc, ncu, g, lds, blocks))
+            return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, lds, blocks, stream, false);
+    }
     g.Pc = p.Pc; g.Qc = p.Qc; g.Kc = p.Kc; g.C = C;
     // Tuning knobs (development sweeps only; defaults are the tuned values).
     static const int knobG = std::getenv("GAR_BG_G") ? std::atoi(std::getenv("GAR_BG_G")) : 0;
@@ -90,55 +216,6 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     g.a_lo = od.o_lo / p.Pc;
     const int64_t a_hi = (od.o_hi + p.Pc - 1) / p.Pc;
     const int64_t nmac = a_hi - g.a_lo;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    // small launch of a row-block-aligned f64 plan (stream chunks): one (column block, row block) per
-    // workgroup, one macro period per column (bg_rb_kernel) -- same programs, same sums
-    if (p.f64 && p.rbAligned && p.rbStart && p.hRbStart && p.nrb <= kBgRbKMaxRb && p.nprog <= kBgRbKMaxProg &&
-        (nmac * C + 15) / 16 <= 2 * static_cast<int64_t>(ncu) && !(knobDbg & 8)) {
-        g.rbMode = 1;
-        for (int i = 0; i <= p.nrb; ++i) g.rbStart[i] = p.hRbStart[i];
-        for (int i = 0; i < p.nprog; ++i) g.rbK0[i] = p.hRbK0[i];
-        g.G = 1;
-        g.W = p.Kc;
-        g.Wl = p.Kread;
-        g.Ws = g.Wl;
-        g.nchunk = static_cast<int>(nmac);
-        g.ncols = static_cast<int>(nmac * C);
-        g.nblocks = (g.ncols + 15) / 16;
-        g.dbg = knobDbg;
-        g.vst = 0;
-        g.parity = 0;
-        g.hdst = nullptr;
-        g.ht0 = g.hn = 0;
-        if (hc && hc->n > 0 && hc->dst) {
-            g.hdst = hc->dst;
-            g.ht0 = hc->t0;
-            g.hn = hc->n;
-            hc->done = true;
-        }
-        // time-major (bg_rt_kernel, knob GAR_BG_RT=0: bg_rb_kernel): workgroups = row blocks x channels
-        // x blocks of 16 consecutive macro periods, each window staged once in LDS
-        // Default: time-major for plans of one or two row blocks (the integer decimator: each window is
-        // staged once; 4800-frame cfg5 calls 26.8 -> 18.9 us), bg_rb_kernel otherwise (a plan of ten row
-        // blocks would stage every window ten times: the cfg5 composite 21.8 -> 33.6 us).
-        static const int knobRt = std::getenv("GAR_BG_RT") ? std::atoi(std::getenv("GAR_BG_RT")) : -1;
-        const size_t rtLds = bgRtLds(p.Qc, p.Kread, p.maxPrb, 8);
-        if ((knobRt == 1 || (knobRt < 0 && p.nrb <= 2)) && rtLds <= 64 * 1024) {
-            g.rbMode = 2;
-            const int64_t nkb = (nmac + 15) / 16;
-            const int64_t blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);
-            return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, rtLds, blocks, stream, false);
-        }
-        const size_t rcLds = bgRcLds(C, p.Qc, p.Kread, p.maxPrb, 8);
-        if (knobRt == 2 && rcLds <= 160 * 1024 - 1024) {
-            g.rbMode = 3;
-            const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
-            return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, rcLds, blocks, stream, false);
-        }
-        const int64_t blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
-        return bgLaunchF64(p.NS, p, src, od, g, 64 * p.maxPrb, 0, blocks, stream, false);
-    }
     const int threads = 64 * g.ncg * g.nwt;
     const int tileN = 16 * g.ncg;
     const size_t slotBytes = static_cast<size_t>(g.ncg) * g.nslots * 256 * sz;

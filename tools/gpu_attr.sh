@@ -17,5 +17,6 @@ KB_CH=${KB_CH:-2} KB_SECONDS=${KB_SECONDS:-600} KB_IN=${KB_IN:-44100} KB_OUT=${K
 python3 -c "
 import json
 for l in open('$O/attr.jsonl'):
-    d=json.loads(l); c=d['cfg']; print('roles', c.get('GAR_HXT_ROLES'), 'dbg', c.get('GAR_HXS_DBG'), 'ms', d.get('ms'), d.get('err','')[-200:])"
+    d=json.loads(l); c=d['cfg']; print('roles', c.get('GAR_HXT_ROLES'), 'dbg', c.get('GAR_HXS_DBG'), 'ms', d.get('ms'), d.get('err','')[-200:])
+    for p in d.get('prof', []): print('    ', p[:260])"
 exit 0
