@@ -461,8 +461,9 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
     for _ in range(warmup):
         step()
     sync()
-    if inline_prof:  # HIP events around every launch inside the timed region (on the launch stream)
-        r.profile(True)
+    if inline_prof:  # HIP events around the FIR launches inside the timed region (on the launch stream);
+        # not around the flush (kind 3, never the dominant kernel): each event pair costs stream time
+        r.profile(True, kinds=(0, 1, 2, 4, 5))
         for k in range(6):
             r.profile_read(k)
     barrier()

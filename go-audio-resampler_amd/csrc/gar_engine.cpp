@@ -644,6 +644,7 @@ struct gar_resampler {
     std::vector<int64_t> scratchSizes;
     // optional HIP-event timing of the MFMA FIR launches (bench.py roofline)
     bool profile = false;
+    uint32_t profileKinds = 0x3f;  // kinds whose launches get events (gar_profile_kinds)
     struct Ev { int tag; hipEvent_t a, b; };
     std::vector<Ev> events;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evPool;
@@ -700,15 +701,17 @@ hipError_t timed(Ctx& x, int tag, L&& launch) {
 
 template <class L>
 hipError_t timedRaw(Ctx& x, int tag, L&& launch) {
-    if (!x.h->profile) return launch();
+    if (!x.h->profile || !((x.h->profileKinds >> tag) & 1u)) return launch();
     hipEvent_t a, b;
     if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
         a = x.h->evPool.back().first;
         b = x.h->evPool.back().second;
         x.h->evPool.pop_back();
     } else {
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
+        // timing events without the system-scope release: a default event's record writes back the
+        // L2 for host visibility, which costs stream time the measured kernel does not own
+        HIPCHK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+        HIPCHK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
     }
     HIPCHK(hipEventRecord(a, x.s));
     const hipError_t e = launch();
@@ -1080,9 +1083,13 @@ int64_t chainProcess(Ctx& x, const InView& in, const OutView& out, std::vector<i
             }
         }
         int64_t m = 0;
-        // decimator -> fused DFT x2 + polyphase (f64): the two launches of this call go out as one
-        // (launchBgPair); knob GAR_BG_PAIR=0 keeps them apart
-        static const bool pairOn = !(std::getenv("GAR_BG_PAIR") && std::getenv("GAR_BG_PAIR")[0] == '0');
+        // decimator -> fused DFT x2 + polyphase (f64): the two launches of a call as one (launchBgPair)
+        // when GAR_BG_PAIR=1 (read per call).  Off by default: measured slower than the two launches
+        // (cfg5 4800-frame calls 37.3 vs 30.4 us of kernel time, profiles/r05b_cfg5_pair.txt) -- the
+        // agent-scope hand-off inside the launch (L2 write-back + invalidate, ~4-8 us) costs more than
+        // the launch boundary it replaces.
+        const char* pk = i + 1 < ns ? std::getenv("GAR_BG_PAIR") : nullptr;
+        const bool pairOn = pk && pk[0] == '1';
         x.deferNext = pairOn && x.launch && x.pend && !last && x.h->f64 && x.h->stages[i]->d.kind == EngineKind::Decim &&
                       x.h->stages[i + 1]->d.kind == EngineKind::DftPoly && x.h->stages[i + 1]->fused &&
                       !x.g->cnt[i + 1].staged;
@@ -1315,7 +1322,10 @@ gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
     gar_status st = wrap([&]() -> gar_status {
         if (h->orderValid && h->lastStream != s) HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
         const gar_status r = f();
-        if (hostSynced) {  // the call synchronised its stream: nothing of it is left to order after
+        // development knob GAR_ORDER_EV=0: no order event per call (measures its stream cost; calls
+        // on different streams are then NOT ordered)
+        static const bool orderEvOff = std::getenv("GAR_ORDER_EV") && std::getenv("GAR_ORDER_EV")[0] == '0';
+        if (hostSynced || orderEvOff) {  // the call synchronised its stream: nothing of it is left to order after
             h->orderValid = false;
         } else {
             HIPCHK(hipEventRecord(h->orderEv, s));
@@ -2097,6 +2107,11 @@ const char* gar_last_error(void) { return g_err.c_str(); }
 void gar_profile_enable(gar_resampler* r, int32_t on) {
     if (!r) return;
     r->profile = on != 0;
+}
+
+void gar_profile_kinds(gar_resampler* r, uint32_t kinds) {
+    if (!r) return;
+    r->profileKinds = kinds & 0x3fu;
 }
 
 gar_status gar_stage_state(const gar_resampler* r, int32_t stage, int32_t* fused_plan, int32_t* fused_now) {

@@ -214,7 +214,14 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     const uintptr_t inA = reinterpret_cast<uintptr_t>(src.in);
     int fmt = 0;
     const bool stereoIl = C == 2 && src.in_fs == 2 && src.in_cs == 1;
-    if (src.in_pcm == 16) {  // PCM16 / PCM24-32 stereo frames; other PCM layouts are gathered
+    if (!src.in) {
+        // no caller input (a flush: history + zeros): every row comes from the history, [t][C] f32 with
+        // row stride hist_ld, so take the load layout from it -- STEREO frames or ROW16 rows -- instead
+        // of per-column element gathers (cfg2's flush launch: 13.7 us on the gathers, r05d trace)
+        const uintptr_t hA = reinterpret_cast<uintptr_t>(src.hist);
+        if (C == 2 && src.hist_ld == 2 && (hA & 7) == 0) fmt = 1;
+        else if (C % 16 == 0 && src.hist_ld % 4 == 0 && (hA & 15) == 0) fmt = 2;
+    } else if (src.in_pcm == 16) {  // PCM16 / PCM24-32 stereo frames; other PCM layouts are gathered
         if ((inA & 3) == 0 && stereoIl) fmt = 3;
     } else if (src.in_pcm) {
         if ((inA & 7) == 0 && stereoIl) fmt = 4;

@@ -44,6 +44,13 @@ constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 #ifndef GAR_HXT_PKLOUD
 #define GAR_HXT_PKLOUD 0
 #endif
+// loader waves' issue priority (s_setprio; 0 = the compute waves' level).  The loaders share each
+// SIMD with three MFMA-issuing compute waves; at equal priority the arbiter lets the MFMA stream
+// starve the loaders' VALU (r05 stamps: ~19 cycles per loader VALU instruction), and the loaders
+// are the kernel's critical path.
+#ifndef GAR_HXT_LPRIO
+#define GAR_HXT_LPRIO 0
+#endif
 constexpr uint32_t kHxtLoudBits = 0x417FF000u;          // bits(kHxLoud = 15.99609375f): !(|x| < kHxLoud) <=> (bits & 0x7fffffff) >= it
 static_assert(__builtin_bit_cast(uint32_t, kHxLoud) == kHxtLoudBits, "hxt's loud test must match hxLoud");
 
@@ -345,6 +352,7 @@ __device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
 template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
                                            int lane, unsigned long long* waited) {
+    if constexpr (GAR_HXT_LPRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXT_LPRIO);
     const HxsArgsP xp = hxsCold();
     const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
     const int P = (Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;

@@ -90,7 +90,7 @@ EXPORTED = [
     "gar_device_flush_size", "gar_reset", "gar_get_ratio", "gar_get_latency", "gar_get_info", "gar_channels",
     "gar_status_string", "gar_last_error", "gar_design_engine", "gar_design_composite", "gar_profile_enable",
     "gar_profile_read", "gar_stage_state", "gar_num_stages", "gar_stage_geometry", "gar_get_statistics",
-    "gar_synchronize", "gar_profile_launch_stats",
+    "gar_synchronize", "gar_profile_launch_stats", "gar_profile_kinds",
 ]
 
 _lib = None
@@ -153,6 +153,7 @@ def lib():
         "gar_stage_geometry": (i32, [vp, i32, C.POINTER(d), C.POINTER(EngineGeometry)]),
         "gar_get_statistics": (i32, [vp, i32, C.POINTER(i64), C.POINTER(i64)]),
         "gar_synchronize": (i32, [vp]),
+        "gar_profile_kinds": (None, [vp, C.c_uint32]),
         "gar_profile_launch_stats": (i32, [vp, i32, C.POINTER(d), C.POINTER(d), C.POINTER(d)]),
     }
     for name, (res, args) in sig.items():
@@ -299,8 +300,10 @@ class Resampler:
         _check(lib().gar_get_info(self._h, C.byref(info)))
         return info
 
-    def profile(self, on=True):
+    def profile(self, on=True, kinds=None):
+        """HIP-event timing of the FIR launches; `kinds` (iterable of kind numbers) limits it."""
         lib().gar_profile_enable(self._h, int(on))
+        lib().gar_profile_kinds(self._h, 0x3F if kinds is None else sum(1 << k for k in kinds))
 
     def profile_read(self, kind=0):
         """(total ms, launches) of one kernel kind (0 fused FIR, 1 DFT FIR, 2 decimator FIR, 3 fused FIR

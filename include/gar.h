@@ -207,6 +207,10 @@ const char *gar_status_string(gar_status s);
 const char *gar_last_error(void);                       /* thread-local detail for the last failure */
 /* HIP-event timing of every MFMA FIR launch (bracketed on its own stream). */
 void gar_profile_enable(gar_resampler *r, int32_t on);
+/* Restricts the event timing to the launch kinds whose bit is set (kind k = bit k, see
+ * gar_profile_read; default all): an event pair costs a few microseconds of stream time, so a
+ * timed region brackets only the kernel it measures. */
+void gar_profile_kinds(gar_resampler *r, uint32_t kinds);
 /* Sum of launch durations (ms) and launch count of one kernel kind (0 fused
  * DFT+polyphase FIR, 1 DFT FIR, 2 decimator FIR, 3 fused FIR launched by a
  * flush, 4 polyphase stage with live cubic coefficients, 5 QualityQuick cubic
