@@ -468,8 +468,14 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
             r.profile_read(k)
     barrier()
     sync()
+    # inline events on every EVENT_EVERY-th step only: an event pair costs a few us of stream time (r05f
+    # trace), so the steps between them run as a caller's would; the kernel average is over the
+    # bracketed launches
+    every = int(os.environ.get("GAR_BENCH_EVENT_EVERY", "4"))
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for k in range(steps):
+        if inline_prof:
+            L.gar_profile_enable(r._h, int(k % every == 0))
         n_proc, n_tail = step()
     sync()
     barrier()
@@ -527,7 +533,8 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
     if not dry:
         roof, kernel_keys = roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail)
         obj["roofline"] = roof
-        roof["kernel_timing"] = ("HIP events around each launch, inside the timed region" if inline_prof
+        roof["kernel_timing"] = ((f"HIP events around the launches of every {int(os.environ.get('GAR_BENCH_EVENT_EVERY', '4'))}th "
+                                  "timed step, inside the timed region, on the launch stream") if inline_prof
                                  else "HIP events around each launch, in a separate pass after the timed steps")
         obj["arith"] = (("int16 PCM I/O converted in the kernel's loads (float64(i)/32767 -> f32) and stores "
                          "(clamp, x32767, truncate); rms_vs_oracle in full-scale units includes the output "

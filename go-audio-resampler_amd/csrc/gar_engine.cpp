@@ -625,6 +625,12 @@ struct gar_resampler {
     hipEvent_t orderEv = nullptr;
     hipStream_t lastStream = nullptr;
     bool orderValid = false;
+    // Recording orderEv costs ~3.5 us of stream time per call (r05f trace: dispatch gaps 7.9 / 8.2 ->
+    // 4.3 / 5.8 us without it), so a handle used on one stream only records none: `unordered` marks
+    // device work not covered by an event.  The first call on a second stream waits for the device
+    // once and turns `multiStream` on; from then on every call records the event.
+    bool unordered = false;
+    bool multiStream = false;
     // a HIP failure mid-call may leave counters advanced past the histories: refuse
     // further work until Reset (ADVICE: no silent wrong output)
     bool poisoned = false;
@@ -1308,6 +1314,15 @@ bool devFault(Handle* h) {
     return true;
 }
 
+// Waits until no device work of the handle's calls is pending (free / reset / synchronize): the
+// order event when one covers the last call, else -- work of single-stream calls left no event --
+// the device (the caller's stream may already be destroyed).
+void drainOrder(Handle* h) {
+    if (h->orderValid) (void)hipEventSynchronize(h->orderEv);
+    else if (h->unordered) (void)hipDeviceSynchronize();
+    h->unordered = false;
+}
+
 template <class F>
 gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
     if (h->poisoned) return guard(GAR_ERR_DEVICE, "handle unusable after an earlier device error; call Reset");
@@ -1320,17 +1335,25 @@ gar_status callOn(Handle* h, hipStream_t s, F&& f, bool hostSynced = false) {
         ~ErrScope() { g_curErr = prev; }
     } es(h->errDev);
     gar_status st = wrap([&]() -> gar_status {
-        if (h->orderValid && h->lastStream != s) HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
+        if (h->orderValid && h->lastStream != s) {
+            HIPCHK(hipStreamWaitEvent(s, h->orderEv, 0));
+        } else if (h->unordered && h->lastStream != s) {  // first switch of stream: earlier calls left no event
+            HIPCHK(hipDeviceSynchronize());
+            h->unordered = false;
+            h->multiStream = true;
+        }
         const gar_status r = f();
-        // development knob GAR_ORDER_EV=0: no order event per call (measures its stream cost; calls
-        // on different streams are then NOT ordered)
-        static const bool orderEvOff = std::getenv("GAR_ORDER_EV") && std::getenv("GAR_ORDER_EV")[0] == '0';
-        if (hostSynced || orderEvOff) {  // the call synchronised its stream: nothing of it is left to order after
+        if (hostSynced) {  // the call synchronised its stream: nothing of it is left to order after
             h->orderValid = false;
-        } else {
+            h->unordered = false;
+        } else if (h->multiStream) {
             HIPCHK(hipEventRecord(h->orderEv, s));
             h->lastStream = s;
             h->orderValid = true;
+        } else {
+            h->lastStream = s;
+            h->orderValid = false;
+            h->unordered = true;
         }
         return r;
     });
@@ -1662,7 +1685,7 @@ void gar_free(gar_resampler* r) {
     DeviceGuard dg(r->dry ? -1 : r->device);
     try {
         if (r->stream) (void)hipStreamSynchronize(r->stream);
-        if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
+        drainOrder(r);
         if (r->orderEv) (void)hipEventDestroy(r->orderEv);
         for (auto& ev : r->events) {
             (void)hipEventDestroy(ev.a);
@@ -1689,6 +1712,8 @@ gar_status gar_synchronize(gar_resampler* r) {
     DeviceGuard dg(r->device);
     const gar_status st = wrap([&]() -> gar_status {
         if (r->orderValid) HIPCHK(hipEventSynchronize(r->orderEv));
+        else if (r->unordered) HIPCHK(hipDeviceSynchronize());
+        r->unordered = false;
         if (r->stream) HIPCHK(hipStreamSynchronize(r->stream));
         return GAR_OK;
     });
@@ -1985,7 +2010,7 @@ void gar_reset(gar_resampler* r) {
             // stream through the event recorded on it, since the caller may have destroyed it)
             if (r->failEvValid) (void)hipEventSynchronize(r->failEv);
             if (r->stream) (void)hipStreamSynchronize(r->stream);
-            if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
+            drainOrder(r);
             (void)hipGetLastError();
             if (r->errHost) __atomic_store_n(r->errHost, 0, __ATOMIC_RELEASE);  // every launch that could write it has drained
             if (r->pairCtr.dev && hipMemset(r->pairCtr.dev, 0, 2 * sizeof(unsigned)) == hipSuccess) r->pairCtr.tick = r->pairCtr.done = 0;
@@ -2012,7 +2037,7 @@ void gar_reset(gar_resampler* r) {
             return;
         }
         if (r->stream) (void)hipStreamSynchronize(r->stream);
-        if (r->orderValid) (void)hipEventSynchronize(r->orderEv);
+        drainOrder(r);
         r->groups.clear();
         r->groups.push_back(freshGroup(r, 0, r->channels));
     } catch (...) {

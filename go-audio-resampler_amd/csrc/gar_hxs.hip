@@ -48,8 +48,11 @@ unsigned long long* profBuf() {
                     if (h[34]) fprintf(stderr, "hxt roles per block (cycles): compute wave 0 %.0f (waiting %.0f), loader 0 %.0f (waiting %.0f), n %llu\n",
                                        static_cast<double>(h[30]) / h[34], static_cast<double>(h[32]) / h[34], static_cast<double>(h[31]) / h[34],
                                        static_cast<double>(h[33]) / h[34], h[34]);
-                    if (h[34]) fprintf(stderr, "hxt compute wave 0: entry -> first group %.0f cycles, last group -> exit %.0f cycles\n",
-                                       static_cast<double>(h[35]) / h[34], static_cast<double>(h[36]) / h[34]);
+                    if (h[34]) fprintf(stderr, "hxt compute wave 0: entry -> first group %.0f cycles, last group -> exit %.0f cycles, periods %.0f, arrivals %.0f\n",
+                                       static_cast<double>(h[35]) / h[34], static_cast<double>(h[36]) / h[34],
+                                       static_cast<double>(h[37]) / h[34], static_cast<double>(h[38]) / h[34]);
+                    if (h[34]) fprintf(stderr, "hxt loader 0 phases (cycles): load data wait %.0f, conversion %.0f, arrival %.0f\n",
+                                       static_cast<double>(h[50]) / h[34], static_cast<double>(h[51]) / h[34], static_cast<double>(h[52]) / h[34]);
                     if (h[44]) fprintf(stderr, "hxq wave 0 (cycles): entry->barrier 1 %.0f, ->image %.0f, ->MFMA+stores issued %.0f, ->drained %.0f, n %llu\n",
                                        static_cast<double>(h[40]) / h[44], static_cast<double>(h[41]) / h[44], static_cast<double>(h[42]) / h[44],
                                        static_cast<double>(h[43]) / h[44], h[44]);

@@ -390,12 +390,27 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                     if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpDone, need, kHxtErrSlotWait, lane, waited);  // development 64: loaders never wait
                     last += GQ;
                 }
+                // development (GAR_HXS_PROF): loader phases of the first block -- waited[3] load data
+                // (an explicit vmcnt wait for this load's instructions), [4] conversion, [5] arrival
+                const bool stp = kHxsDev && waited;
+                unsigned long long t1 = stp ? __builtin_amdgcn_s_memtime() : 0;
+                if (stp && fastL[d]) {
+                    constexpr int kNewer = (FMT == 1 ? 2 : 1) * hxtItems<NL>() * (kHxtD - 1);  // younger loads' instructions
+                    static_assert(kNewer < 64, "vmcnt field");
+                    __builtin_amdgcn_s_waitcnt((kNewer & 15) | (7 << 4) | (15 << 8) | ((kNewer >> 4) << 14));
+                    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+                    waited[3] += t2 - t1;
+                    t1 = t2;
+                }
                 if (!((dbg & 16) && j >= P)) {
                     const HxsStage st = stage(j);
                     if (fastL[d]) hxtConvert<FMT, NL>(x, st, uni(p0), buf[d], b, l, lane, sh);
                     else hxtGatherLoad(xp, st, b, l, NL, lane, sh);
                 }
+                unsigned long long t3 = stp ? __builtin_amdgcn_s_memtime() : 0;
+                if (stp) waited[4] += t3 - t1;
                 hxtArrive(sy.ldArr, sy.ldDone, j, NL, lane);
+                if (stp) waited[5] += __builtin_amdgcn_s_memtime() - t3;
                 p0 += GQ;
                 if (p0 >= R) p0 -= R;
             }
@@ -449,7 +464,11 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
             if (!(dbg & 32)) hxtWait(x, sy, sy.ldDone, P + g + x.faultNeed, kHxtErrLoadWait, lane, st);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
-            if (kHxsDev && st && st[1] == 0) st[1] = __builtin_amdgcn_s_memtime();
+            if (kHxsDev && st) {
+                const unsigned long long tg = __builtin_amdgcn_s_memtime();
+                if (st[1] == 0) st[1] = tg;
+                st[5] = tg;  // this group's compute starts
+            }
             // the lane's ring offset, recomputed per group (a value held across the group loop spills,
             // and its reload's vmcnt(0) would wait for this wave's output stores)
             int ln = lane;
@@ -486,7 +505,10 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
                 aH = aN;
             }
         }
+        const unsigned long long ta = (kHxsDev && st) ? __builtin_amdgcn_s_memtime() : 0;
+        if (kHxsDev && st && n > 0) st[3] += ta - st[5];  // the group's periods (B reads, MFMA, epilogues)
         hxtArrive(sy.cpArr, sy.cpDone, g, x.ncomp, lane);  // this wave's reads of group g's window are done
+        if (kHxsDev && st) st[4] += __builtin_amdgcn_s_memtime() - ta;
     }
     if (kHxsDev && st) st[2] = __builtin_amdgcn_s_memtime();
 }
@@ -557,7 +579,7 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     const bool stampW = kHxsDev && x.prof && lane == 0 && (wt == 0 || wt == x.ncomp);
     const unsigned long long tEntry = stampW ? __builtin_amdgcn_s_memtime() : 0;
     const unsigned long long rEntry = stampW ? __builtin_amdgcn_s_memrealtime() : 0;
-    unsigned long long st[3] = {0, 0, 0};
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tBlockEnd = 0;
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
@@ -589,6 +611,8 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
         if (wt == 0) {
             atomicAdd(x.prof + 30, tBlockEnd - tEntry);
             atomicAdd(x.prof + 32, st[0]);
+            atomicAdd(x.prof + 37, st[3]);
+            atomicAdd(x.prof + 38, st[4]);
             atomicAdd(x.prof + 34, 1ull);
             atomicAdd(x.prof + 35, st[1] ? st[1] - tEntry : 0ull);  // entry -> first group runs (fill)
             atomicAdd(x.prof + 36, tExit - (st[2] ? st[2] : tExit));  // last group done -> exit (drain)
@@ -598,6 +622,9 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
         } else {
             atomicAdd(x.prof + 31, tBlockEnd - tEntry);
             atomicAdd(x.prof + 33, st[0]);
+            atomicAdd(x.prof + 50, st[3]);
+            atomicAdd(x.prof + 51, st[4]);
+            atomicAdd(x.prof + 52, st[5]);
         }
     }
 }
