@@ -51,6 +51,9 @@ unsigned long long* profBuf() {
                     if (h[34]) fprintf(stderr, "hxt compute wave 0: entry -> first group %.0f cycles, last group -> exit %.0f cycles, periods %.0f, arrivals %.0f\n",
                                        static_cast<double>(h[35]) / h[34], static_cast<double>(h[36]) / h[34],
                                        static_cast<double>(h[37]) / h[34], static_cast<double>(h[38]) / h[34]);
+                    if (h[34] && h[57]) fprintf(stderr, "hxt fill (cycles): entry -> A issued %.0f, -> fill barrier %.0f, -> first group %.0f; in-kernel clock %.3f GHz\n",
+                                       static_cast<double>(h[53]) / h[34], static_cast<double>(h[54]) / h[34], static_cast<double>(h[55]) / h[34],
+                                       0.1 * static_cast<double>(h[56]) / static_cast<double>(h[57]));
                     if (h[34]) fprintf(stderr, "hxt loader 0 phases (cycles): load data wait %.0f, conversion %.0f, arrival %.0f\n",
                                        static_cast<double>(h[50]) / h[34], static_cast<double>(h[51]) / h[34], static_cast<double>(h[52]) / h[34]);
                     if (h[44]) fprintf(stderr, "hxq wave 0 (cycles): entry->barrier 1 %.0f, ->image %.0f, ->MFMA+stores issued %.0f, ->drained %.0f, n %llu\n",
@@ -334,6 +337,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.err = od.err;
     x.pollMax = 1 << 24;
     x.faultNeed = 0;
+    static const int knobCoop = std::getenv("GAR_HXT_COOP") ? std::atoi(std::getenv("GAR_HXT_COOP")) : 1;
+    x.coop = knobCoop;
     if (hxt) {
         const char* f = std::getenv("GAR_HXT_FAULT");
         if (f && f[0] == '1') {

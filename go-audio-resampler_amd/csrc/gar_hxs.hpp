@@ -108,6 +108,7 @@ struct HxsArgs {
     int* err;               // the handle's device status word (host-mapped), written when a progress wait expires
     int pollMax;            // progress-wait bound in polls (2^24; development knob GAR_HXT_FAULT: 2^12)
     int faultNeed;          // development (GAR_HXT_FAULT=1): added to the compute waves' load count, unreachable
+    int coop;               // hxt_kernel: compute waves stage each block's first window (GAR_HXT_COOP=0: loaders)
     // hxq_kernel (small f32 STEREO / ROW16 launches): workgroup = (block, qRbs row blocks), qGroups per block
     int qRbs, qGroups;
     int qU0[12], qRbw[12];  // first window row / row block of each row-block program (HxDev::hU0)

@@ -38,12 +38,6 @@ __host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL)
 // FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row).
 template <int NL>
 constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
-#ifndef GAR_HXT_UPUT
-#define GAR_HXT_UPUT 0
-#endif
-#ifndef GAR_HXT_PKLOUD
-#define GAR_HXT_PKLOUD 0
-#endif
 // loader waves' issue priority (s_setprio; 0 = the compute waves' level).  The loaders share each
 // SIMD with three MFMA-issuing compute waves; at equal priority the arbiter lets the MFMA stream
 // starve the loaders' VALU (r05 stamps: ~19 cycles per loader VALU instruction), and the loaders
@@ -187,6 +181,13 @@ __device__ GAR_HXT_SLOW_ATTR void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b,
 }
 
 // Fast load `st` -> ring (registers of its issue): split, write, one running max for the loud test.
+// GAR_HXT_SPLITFIRST (default): every item's f16 split first, as one branch-free block the scheduler
+// interleaves across items, then the ring writes (their per-item / per-lane conditions are branches);
+// split and write per item inside the branches (0) left each item's dependent VALU chain alone in its
+// basic block (r05 stamps: ~730 cycles per item on a loader beside three MFMA waves).
+#ifndef GAR_HXT_SPLITFIRST
+#define GAR_HXT_SPLITFIRST 1
+#endif
 template <int FMT, int NL>
 __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st, int p0, const HxtBuf<FMT, NL>& r, int b,
                                            int l, int lane, const HxsShared& sh) {
@@ -197,88 +198,89 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
     // (ten live row registers spill, and every reload's vmcnt(0) waits for the loads in flight)
     int ln = lane, lq = l;
     asm volatile("" : "+v"(ln), "+s"(lq));
-    uint32_t m = 0, mh = 0;
+    uint32_t m = 0;
+    auto itemPos = [&](int k, int& row, int& q) {  // -> whether item k holds rows of this load (uniform)
+        if constexpr (FMT == 1) {
+            const int it = lq + NL * k, pc = it >> 2;
+            row = 64 * pc + ln;
+            q = it & 3;
+            return pc < hxtPieces(NL) && 64 * pc < nrow;
+        } else {
+            const int it = lq + NL * k;
+            row = 16 * it + (ln & 15);
+            q = ln >> 4;
+            return 16 * it < nrow;
+        }
+    };
+#if GAR_HXT_SPLITFIRST
+    // in chunks of kSplitChunk items: the split values of a chunk stay within the registers the
+    // consumed load buffer frees (a whole load's at once spilled on FMT 2)
+    constexpr int K = hxtItems<NL>(), kSplitChunk = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += kSplitChunk) {
+        uint2 hv[kSplitChunk], lv[kSplitChunk];
+#pragma unroll
+        for (int u = 0; u < kSplitChunk; ++u) {  // items the load does not hold were loaded as zeros
+            if (k0 + u >= K) break;
+            const f32x4 e = hxtItem<FMT, NL>(r, k0 + u);
+            m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
+            hxSplit2(e[0], e[1], hv[u].x, lv[u].x);
+            hxSplit2(e[2], e[3], hv[u].y, lv[u].y);
+        }
+#pragma unroll
+        for (int u = 0; u < kSplitChunk; ++u) {
+            if (k0 + u >= K) break;
+            int row, q;
+            if (itemPos(k0 + u, row, q) && row < nrow) {
+                int p = p0 + row;
+                p = p >= R ? p - R : p;
+                uint32_t qs = sh.QS;  // quad base recomputed per item (opaque): hoisted per-quad bases spill
+                asm volatile("" : "+s"(qs));
+                char* qb = sh.ring + q * qs;
+                *reinterpret_cast<uint2*>(qb + 8 * p) = hv[u];
+                *reinterpret_cast<uint2*>(qb + dL + 8 * p) = lv[u];
+                if (p < mirror) {
+                    *reinterpret_cast<uint2*>(qb + 8 * (p + R)) = hv[u];
+                    *reinterpret_cast<uint2*>(qb + dL + 8 * (p + R)) = lv[u];
+                }
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < hxtItems<NL>(); ++k) {
         int row, q;
-        bool on;
-        if constexpr (FMT == 1) {
-            const int it = lq + NL * k, pc = it >> 2;
-            on = pc < hxtPieces(NL) && 64 * pc < nrow;
-            row = 64 * pc + ln;
-            q = it & 3;
-        } else {
-            const int it = lq + NL * k;
-            on = 16 * it < nrow;
-            row = 16 * it + (ln & 15);
-            q = ln >> 4;
-        }
-        if (on) {  // uniform
+        if (itemPos(k, row, q)) {  // uniform
             const f32x4 e = hxtItem<FMT, NL>(r, k);
-#if GAR_HXT_PKLOUD  // loud <=> the f16 hi half overflows (kHxLoud is exactly that bound): packed u16 max
-            {
-                uint32_t h0, l0, h1, l1;
-                hxSplit2(e[0], e[1], h0, l0);
-                hxSplit2(e[2], e[3], h1, l1);
-                typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-                u16x2 mm = __builtin_bit_cast(u16x2, mh);
-                mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, h0 & 0x7fff7fffu));
-                mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, h1 & 0x7fff7fffu));
-                mh = __builtin_bit_cast(uint32_t, mm);
-                (void)l0; (void)l1;
-            }
-#else
             m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
-#endif
             int p = p0 + row;
             p = p >= R ? p - R : p;
-            // quad base recomputed per item (opaque): eight hoisted per-quad bases spill to VGPR lanes
             uint32_t qs = sh.QS;
             asm volatile("" : "+s"(qs));
-#if GAR_HXT_UPUT  // A/B: the mirror copy decided per 64-row piece (uniform) except at the mirror's end
-            if (row < nrow) {
-                char* qb = sh.ring + q * qs;
-                uint2 hv, lv;
-                hxSplit2(e[0], e[1], hv.x, lv.x);
-                hxSplit2(e[2], e[3], hv.y, lv.y);
-                *reinterpret_cast<uint2*>(qb + 8 * p) = hv;
-                *reinterpret_cast<uint2*>(qb + dL + 8 * p) = lv;
-                constexpr int kPiece = FMT == 1 ? 64 : 16;
-                const int pLo = uni(p0 + kPiece * (FMT == 1 ? (lq + NL * k) >> 2 : lq + NL * k));  // piece's first ring row, unwrapped
-                const bool none = pLo >= mirror && pLo + kPiece <= R;  // uniform: no row of the piece in [0, mirror)
-                const bool all = pLo + kPiece <= mirror;               // uniform: every row of it
-                if (!none && (all || p < mirror)) {
-                    *reinterpret_cast<uint2*>(qb + 8 * (p + R)) = hv;
-                    *reinterpret_cast<uint2*>(qb + dL + 8 * (p + R)) = lv;
-                }
-            }
-#else
             if (row < nrow) hxtPut(sh.ring + q * qs, dL, p, R, mirror, e);
-#endif
         }
     }
-#if GAR_HXT_PKLOUD
-    m = ((mh & 0xffffu) >= 0x7c00u || (mh >> 16) >= 0x7c00u) ? kHxtLoudBits : 0u;
 #endif
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
         hxtLoudLoad<FMT, NL>(hxsCold(), st, b, l, lane, sh);
 }
 
 // ---- progress counters (LDS) -------------------------------------------------------------
-// Inside a block no workgroup barrier is taken.  Two monotone counters carry the hand-offs:
-// ldDone = loads converted by EVERY loader, cpDone = groups finished by EVERY compute wave.
-// Group g may run once ldDone >= P+g (its window, loads 0 .. P+g-1); load j may overwrite ring
-// rows once cpDone reaches the last group whose window held them (hxtFreeNeed).
-// Each counter is advanced by the last of its producers to arrive: a producer that is done with
-// load j / group g adds 1 to the arrival slot arr[j % kHxtSlots] (ds_add_rtn, lane 0 only) and the
-// one that completes the count writes done = j + 1.  Producers finish their items in order, so the
-// last arrival at j also means every producer is done with everything before j, and `done` only
-// grows.  A producer can run at most (ring slots + 2) loads / groups ahead of the slowest one
-// (host check hxtSlotsOk), so slot j % kHxtSlots never holds arrivals of two laps at once.
+// Inside a block no workgroup barrier is taken.  A producer that is done with item j (a loader with
+// load j, a compute wave with group g) adds 1 to the arrival slot arr[j % kHxtSlots] -- lane 0, a
+// non-returning ds_add (round 5 first had the last arriver read the sum back and publish a done word:
+// the returning atomic's latency behind the LDS queue cost every wave ~1.5k cycles per arrival, 10 %
+// of its life in the stamps).  Item j is complete once its slot holds n * (j / kHxtSlots + 1)
+// arrivals of its n producers.  Producers finish their items in order, so a complete item also
+// means every earlier item is complete, and a waiter checks only the last item it needs: group g
+// runs once load P+g-1 is complete (its window: loads 0 .. P+g-1); load j may overwrite ring rows
+// once the last group whose window held them is complete (hxtFreeNeed).  A producer runs at most
+// (ring slots + 2) items ahead of the slowest one (host check in launchHxs), fewer than kHxtSlots,
+// so a slot never holds arrivals of two laps at once and a count never runs past n * (lap + 1).
 // A producer arrives after s_waitcnt lgkmcnt(0) (its ring writes / reads done), and LDS executes
-// one wave's operations in order, so a waiter that sees `done` and then reads the ring sees the
-// data.  A waiter polls one dword (broadcast ds_read_b32, s_sleep backoff) -- round 4 polled
-// every producer's own counter with two or three ds_read_b128 per poll.
+// one wave's operations in order, so a waiter that sees the count and then reads the ring sees the
+// data.  A waiter polls one dword (broadcast ds_read_b32, s_sleep backoff) -- round 4 polled every
+// producer's own counter with two or three ds_read_b128 per poll.
 // Waits are bounded (x.pollMax polls): an expired wait means a counting bug, so the wave records
 // it in the workgroup's abort word (every later wait of the workgroup returns at once, the grid
 // drains) and in the handle's device status word x.err (host-mapped; the C-ABI reports
@@ -290,30 +292,31 @@ constexpr int kHxtSlots = 16;                            // arrival slots per di
 struct HxtSync {
     lds_i32* ldArr;   // [kHxtSlots] loader arrivals per load
     lds_i32* cpArr;   // [kHxtSlots] compute-wave arrivals per group
-    lds_i32* ldDone;  // loads converted by every loader
-    lds_i32* cpDone;  // groups finished by every compute wave
     lds_i32* abort;   // a wait of this workgroup expired (sticky for the launch)
 };
 // LDS bytes past loudLo (hxsLds reserves them): loudLo[16], loudHi[16], flag, then the counters
 constexpr int kHxtSyncOff = 160;
-constexpr int kHxtSyncBytes = 4 * (2 * kHxtSlots + 3);
+constexpr int kHxtSyncBytes = 4 * (2 * kHxtSlots + 1);
 
-// Producer arrival for item j (load or group) of `n` producers.
-__device__ __forceinline__ void hxtArrive(lds_i32* arr, lds_i32* done, int j, int n, int lane) {
+// Producer arrival for item j.
+__device__ __forceinline__ void hxtArrive(lds_i32* arr, int j, int lane) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring writes / reads done
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) {
-        const int prev = __hip_atomic_fetch_add(arr + (j & (kHxtSlots - 1)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (prev == (j / kHxtSlots) * n + n - 1) *reinterpret_cast<volatile lds_i32*>(done) = j + 1;
-    }
+    if (lane == 0) (void)__hip_atomic_fetch_add(arr + (j & (kHxtSlots - 1)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// *done >= need, bounded; on expiry the abort word and the handle's status word are set.
-__device__ __forceinline__ void hxtWait(const HxsArgs& x, const HxtSync& sy, const lds_i32* done, int need, int code,
+__device__ __forceinline__ bool hxtComplete(const lds_i32* arr, int j, int n) {
+    return *reinterpret_cast<const volatile lds_i32*>(arr + (j & (kHxtSlots - 1))) >= n * (j / kHxtSlots + 1);
+}
+
+// Item j (of n producers) complete, bounded; on expiry the abort word and the handle's status word
+// are set.  j < 0: nothing to wait for.
+__device__ __forceinline__ void hxtWait(const HxsArgs& x, const HxtSync& sy, const lds_i32* arr, int j, int n, int code,
                                         int lane, unsigned long long* waited = nullptr) {
+    if (j < 0) return;
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (*reinterpret_cast<const volatile lds_i32*>(done) >= need) return;  // the common case: one read
+    if (hxtComplete(arr, j, n)) return;                                    // the common case: one read
     if (*reinterpret_cast<const volatile lds_i32*>(sy.abort)) return;      // after an expiry: no more waiting
     const unsigned long long t0 = (kHxsDev && waited) ? __builtin_amdgcn_s_memtime() : 0;
     struct Acc {  // development (GAR_HXS_PROF): cycles spent in this wait
@@ -326,7 +329,7 @@ __device__ __forceinline__ void hxtWait(const HxsArgs& x, const HxtSync& sy, con
     for (; it < pmax; ++it) {
         __builtin_amdgcn_s_sleep(1);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (*reinterpret_cast<const volatile lds_i32*>(done) >= need) break;
+        if (hxtComplete(arr, j, n)) break;
         if (*reinterpret_cast<const volatile lds_i32*>(sy.abort)) { it = pmax; break; }
     }
     if (it >= pmax) {  // expired (here or in another wave of the workgroup): record, stop waiting
@@ -349,9 +352,63 @@ __device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
 // Loader wave l: in step j it waits for the ring rows of load j to be free, converts load j
 // (issued kHxtD steps earlier) into the ring, publishes it and issues load j + kHxtD into the
 // registers just freed.
+// Block b's first window (rows [0, Wg), i.e. loads 0 .. P-1) can come through the buffer records
+// (uniform): every column live and the window at or after the raw input's first row.
+__device__ __forceinline__ bool hxtStage0Fast(const HxsArgs& x, int b) {
+    const bool blockLive = x.fmt >= 1 && x.fmt <= 2 && b * 16 + 15 < x.ncols && x.fastHi > x.fastLo;
+    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * 16) / x.C) * x.Np) * x.Qc;
+    return blockLive && row0 >= x.fastLo;
+}
+
+// Cooperative fill: the compute waves (idle until the first window is in the ring) load and convert
+// the block's first window together -- one memory round trip of the whole workgroup -- instead of the
+// loaders staging loads 0 .. P-1 one loader step after another (r05 stamps: entry -> first group was
+// ~45k cycles, 15 % of a cfg2 workgroup's life).  Items as the loaders' (FMT 1: quad + 64-row piece,
+// two chunks of stereo frames; FMT 2: 16-row piece, lane = 16 quad + row), kCoopB in flight per
+// wave, each staged through hxsPutItem (split, mirror, loud marking) like the edge gathers.
+template <int FMT>
+__device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared& sh, int b, int w, int nw, int lane) {
+    const HxsArgsP xp = hxsCold();
+    const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
+    HxsStage st;
+    st.T0 = 0;
+    st.nrow = x.Wg;
+    st.fast = true;
+    const int Wg = x.Wg;
+    const int nit = FMT == 1 ? 4 * ((Wg + 63) >> 6) : (Wg + 15) >> 4;
+    constexpr int kCoopB = 4;
+    for (int it0 = w; it0 < nit; it0 += kCoopB * nw) {
+        f32x4 e[kCoopB];
+#pragma unroll
+        for (int u = 0; u < kCoopB; ++u) {
+            const int it = it0 + u * nw;
+            const bool on = it < nit;
+            if constexpr (FMT == 1) {
+                const int q = it & 3, pc = it >> 2;
+                const int o = on ? rs.lane0 + 64 * pc * rs.rowB + 2 * q * rs.chunkB : kHxqOob;
+                const int o2 = on ? o + rs.chunkB : kHxqOob;
+                const f2v a = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
+                const f2v c = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
+                e[u] = f32x4{a.x, a.y, c.x, c.y};
+            } else {
+                const int o = on ? rs.lane0 + 16 * it * rs.rowB : kHxqOob;
+                e[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCoopB; ++u) {
+            const int it = it0 + u * nw;
+            if (it >= nit) continue;  // uniform
+            const int q = FMT == 1 ? (it & 3) : (lane >> 4);
+            const int row = FMT == 1 ? 64 * (it >> 2) + lane : 16 * it + (lane & 15);
+            if (row < Wg) hxsPutItem(xp, st, 0, q, row, e[u], sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
+        }
+    }
+}
+
 template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
-                                           int lane, unsigned long long* waited) {
+                                           int lane, bool coop, unsigned long long* waited) {
     if constexpr (GAR_HXT_LPRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXT_LPRIO);
     const HxsArgsP xp = hxsCold();
     const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
@@ -374,12 +431,16 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     HxtBuf<FMT, NL> buf[kHxtD];
     bool fastL[kHxtD];
     const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
+    // with the cooperative fill the compute waves stage loads 0 .. P-1: the loaders start at P, with
+    // its loads in flight across the fill's barrier
+    const int jStart = coop ? P : 0;
 #pragma unroll
-    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(d), d < nL, rs, l, buf[d]);
+    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(jStart + d), jStart + d < nL, rs, l, buf[d]);
+    if (coop) hxsBarrier();  // the first window is in the ring (no vector-memory wait: the loads stay in flight)
     // ring row of load j's first row (incremental: T0 % R) and the groups its rows' previous
     // occupants belong to (hxtFreeNeed, incremental)
-    int p0 = 0, last = Wg + GQ - 1 - R, need = 0;
-    for (int j0 = 0; j0 < nstepsPad; j0 += kHxtD) {
+    int p0 = coop ? Wg : 0, last = Wg + GQ - 1 - R, need = 0;
+    for (int j0 = jStart; j0 < nstepsPad; j0 += kHxtD) {
 #pragma unroll
         for (int d = 0; d < kHxtD; ++d) {
             const int j = j0 + d;
@@ -387,7 +448,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (j >= P) {
                     if (j == P) p0 = Wg;  // Wg < R
                     need = last < 0 ? 0 : need + 1;
-                    if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpDone, need, kHxtErrSlotWait, lane, waited);  // development 64: loaders never wait
+                    if (need > 0 && !(dbg & 64)) hxtWait(x, sy, sy.cpArr, need - 1, x.ncomp, kHxtErrSlotWait, lane, waited);  // development 64: loaders never wait
                     last += GQ;
                 }
                 // development (GAR_HXS_PROF): loader phases of the first block -- waited[3] load data
@@ -409,7 +470,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 }
                 unsigned long long t3 = stp ? __builtin_amdgcn_s_memtime() : 0;
                 if (stp) waited[4] += t3 - t1;
-                hxtArrive(sy.ldArr, sy.ldDone, j, NL, lane);
+                hxtArrive(sy.ldArr, j, lane);
                 if (stp) waited[5] += __builtin_amdgcn_s_memtime() - t3;
                 p0 += GQ;
                 if (p0 >= R) p0 -= R;
@@ -427,7 +488,7 @@ template <int NS, int VST, bool FAST>
 __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int wt, int lane,
                                           const h8v (&Ah)[NS], const h8v (&Al)[NS], uint32_t laneOff, int u0, int P,
                                           int nslot, const HxtRole& ro, char* obase, int64_t pstride, int64_t aCol,
-                                          int64_t oRow0, bool colOk, int ccol, bool fullRb, unsigned long long* st) {
+                                          int64_t oRow0, bool colOk, int ccol, bool fullRb, int nl, unsigned long long* st) {
     // st (development, GAR_HXS_PROF): [0] cycles waiting for loads, [1] first group's start, [2] last group's end
     const int sh = -(x.ea + kHxXs);
     const int GQ = x.G * x.Qc;
@@ -463,7 +524,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         while (first < p0) first += ro.st;
         const int n = first >= pend ? 0 : (pend - first + ro.st - 1) / ro.st;
         if (n > 0) {
-            if (!(dbg & 32)) hxtWait(x, sy, sy.ldDone, P + g + x.faultNeed, kHxtErrLoadWait, lane, st);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
+            if (!(dbg & 32)) hxtWait(x, sy, sy.ldArr, P + g - 1 + x.faultNeed, nl, kHxtErrLoadWait, lane, st);  // loads 0 .. P+g-1 in the ring (development 32: no wait)
             if (kHxsDev && st) {
                 const unsigned long long tg = __builtin_amdgcn_s_memtime();
                 if (st[1] == 0) st[1] = tg;
@@ -507,15 +568,15 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
         }
         const unsigned long long ta = (kHxsDev && st) ? __builtin_amdgcn_s_memtime() : 0;
         if (kHxsDev && st && n > 0) st[3] += ta - st[5];  // the group's periods (B reads, MFMA, epilogues)
-        hxtArrive(sy.cpArr, sy.cpDone, g, x.ncomp, lane);  // this wave's reads of group g's window are done
+        hxtArrive(sy.cpArr, g, lane);  // this wave's reads of group g's window are done
         if (kHxsDev && st) st[4] += __builtin_amdgcn_s_memtime() - ta;
     }
     if (kHxsDev && st) st[2] = __builtin_amdgcn_s_memtime();
 }
 
-template <int NS, int VST>
+template <int NS, int VST, int FMT>
 __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int b, int wt,
-                                           int lane, unsigned long long* st) {
+                                           int lane, int nl, bool coop, unsigned long long* st) {
     // A of the wave's row block (kept in registers only inside this role: the loaders' registers
     // are the load buffers)
     const HxtRole ro = hxtRole(x, wt);
@@ -527,6 +588,12 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
         Ah[i] = x.A[((static_cast<size_t>(ro.rb) * NS + i) * 2 + 0) * 64 + lane];
         Al[i] = x.A[((static_cast<size_t>(ro.rb) * NS + i) * 2 + 1) * 64 + lane];
     }
+    if (kHxsDev && st) st[6] = __builtin_amdgcn_s_memtime();
+    if (coop) {  // the block's first window, staged by every compute wave (A lands meanwhile)
+        hxtCoopStage0<FMT>(x, sh_, b, wt, x.ncomp, lane);
+        hxsBarrier();
+    }
+    if (kHxsDev && st) st[7] = __builtin_amdgcn_s_memtime();
     const uint32_t QS = sh_.QS;
     const int GQ = x.G * x.Qc;
     const int grp = lane >> 4, l16 = lane & 15;
@@ -546,10 +613,10 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
                   (VST == 2 ? 0 : ccol * x.out_cs);
     if (__builtin_amdgcn_ballot_w64(!laneFast) == 0)
         hxtGroups<NS, VST, true>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                 colOk, ccol, fullRb, st);
+                                 colOk, ccol, fullRb, nl, st);
     else
         hxtGroups<NS, VST, false>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                  colOk, ccol, fullRb, st);
+                                  colOk, ccol, fullRb, nl, st);
 }
 
 // FMT: 1 stereo f32 frames, 2 rows of 16 f32 channels.  VST: 0 any f32 layout, 1 channel-contiguous
@@ -568,9 +635,7 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     // kHxtSyncOff B past loudLo (hxsLds reserves the space past the ring): arrival slots, done counters, abort
     sy.ldArr = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + kHxtSyncOff);
     sy.cpArr = sy.ldArr + kHxtSlots;
-    sy.ldDone = sy.cpArr + kHxtSlots;
-    sy.cpDone = sy.ldDone + 1;
-    sy.abort = sy.cpDone + 1;
+    sy.abort = sy.cpArr + kHxtSlots;
     const int lane = threadIdx.x & 63;
     const int wt = uni(threadIdx.x >> 6);
     const bool comp = wt < x.ncomp;
@@ -588,13 +653,16 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
             s.loudLo[threadIdx.x] = INT_MAX;
             s.loudHi[threadIdx.x] = -1;
         }
-        if (threadIdx.x < 2 * kHxtSlots + 2) sy.ldArr[threadIdx.x] = 0;  // arrivals, ldDone, cpDone
+        // cooperative fill (knob x.coop): loads 0 .. P-1 complete once the fill's barrier passes
+        const int GQb = x.G * x.Qc, Pb = (x.Wg + GQb - 1) / GQb;
+        const bool coop = x.coop && hxtStage0Fast(x, b);
+        if (threadIdx.x < 2 * kHxtSlots) sy.ldArr[threadIdx.x] = (coop && static_cast<int>(threadIdx.x) < Pb) ? NL : 0;  // arrival slots
         if (threadIdx.x == 64) *s.flag = 0;
         __syncthreads();
         const bool first = bi == static_cast<int>(blockIdx.x);
         unsigned long long* stp = (stampW && first) ? st : nullptr;
-        if (comp) hxtCompute<NS, VST>(x, s, sy, b, wt, lane, stp);
-        else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane, stp);
+        if (comp) hxtCompute<NS, VST, FMT>(x, s, sy, b, wt, lane, NL, coop, stp);
+        else hxtLoaders<FMT, NL>(x, s, sy, b, wt - x.ncomp, lane, coop, stp);
         if (stampW && first) tBlockEnd = __builtin_amdgcn_s_memtime();
         __syncthreads();  // every wave's part of the block done; flag final
         if (*s.flag) {  // uniform
@@ -616,6 +684,11 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
             atomicAdd(x.prof + 34, 1ull);
             atomicAdd(x.prof + 35, st[1] ? st[1] - tEntry : 0ull);  // entry -> first group runs (fill)
             atomicAdd(x.prof + 36, tExit - (st[2] ? st[2] : tExit));  // last group done -> exit (drain)
+            atomicAdd(x.prof + 53, st[6] - tEntry);  // fill parts: entry -> A issued
+            atomicAdd(x.prof + 54, st[7] - st[6]);  // -> cooperative fill's barrier passed
+            atomicAdd(x.prof + 55, st[1] ? st[1] - st[7] : 0ull);  // -> first group runs
+            atomicAdd(x.prof + 56, tExit - tEntry);  // in-kernel clock: memtime / memrealtime x 100 MHz
+            atomicAdd(x.prof + 57, rExit - rEntry);
             atomicMin(x.prof + 10, rEntry);
             atomicMax(x.prof + 11, rExit);
             if (blockIdx.x < 4096) { x.prof[64 + 2 * blockIdx.x] = rEntry; x.prof[65 + 2 * blockIdx.x] = rExit - rEntry; }

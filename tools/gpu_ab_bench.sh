@@ -2,7 +2,7 @@
 # One GPU call: selected GPU tests, then bench lines for WORKLOADS under each env setting in ABS
 # (space-separated NAME=VALUE[,NAME=VALUE] groups; "-" = defaults).  Stops at the first failure.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/ab
+O=$R/gpurun_out/${TAG:-abb}
 mkdir -p $O
 if [ -z "$NO_TESTS" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-500} python -u -m pytest -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
