@@ -9,8 +9,10 @@
 // interleaved [t][channel] rows and all sample arithmetic runs in HIP kernels
 // (gar_kernels.hip).  Channels in lockstep share one group and one launch.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -21,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "gar.h"
@@ -498,7 +501,10 @@ struct HostBuf {
 };
 
 // Host worker pool for packing / unpacking large host C-ABI calls (one job split over
-// min(15, cores - 1) workers + the caller); small calls run inline.
+// min(15, cores - 1) workers + the caller); small calls run inline.  Workers spin for ~100 us
+// after a job before sleeping (a streaming host call hands the pool two jobs, pack and unpack, a few
+// hundred microseconds apart; a futex wake per job and worker cost tens of microseconds), and job
+// completion is an atomic count.
 class Pool {
    public:
     static Pool& get() {
@@ -513,18 +519,21 @@ class Pool {
             for (int i = 0; i < n; ++i) f(i);
             return;
         }
-        std::unique_lock<std::mutex> lk(mu_);
-        job_ = &f;
-        njobs_ = n;
-        next_.store(0);
-        pending_ = n;
-        ++gen_;
-        cv_.notify_all();
-        lk.unlock();
-        work();
-        lk.lock();
-        done_.wait(lk, [&] { return pending_ == 0; });
-        job_ = nullptr;
+        uint64_t g;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_.store(&f);
+            njobs_.store(n);
+            pending_.store(n);
+            g = (ticket_.load() >> 32) + 1;
+            ticket_.store(g << 32);  // publishes the job: generation g, next index 0
+            cv_.notify_all();
+        }
+        work(g);
+        if (!spinUntil([&] { return pending_.load() == 0; })) {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_.wait(lk, [&] { return pending_.load() == 0; });
+        }
     }
     int workers() const { return static_cast<int>(th_.size()) + 1; }
 
@@ -537,45 +546,62 @@ class Pool {
     ~Pool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
+            stop_.store(true);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
-    void work() {
+    template <class P>
+    static bool spinUntil(P pred) {  // up to ~100 us
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0;; ++k) {
+            if (pred()) return true;
+            _mm_pause();
+            if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) return false;
+        }
+    }
+    // Claims indices of generation g only (a worker that woke late for a finished job must not
+    // take an index of the next one: compare-and-swap on the (generation, index) ticket).
+    void work(uint64_t g) {
         for (;;) {
-            const int i = next_.fetch_add(1);
-            if (i >= njobs_) return;
-            (*job_)(i);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_all();
+            uint64_t t = ticket_.load();
+            for (;;) {
+                if ((t >> 32) != g || static_cast<int64_t>(t & 0xffffffffu) >= njobs_.load()) return;
+                if (ticket_.compare_exchange_weak(t, t + 1)) break;
+            }
+            (*job_.load())(static_cast<int>(t & 0xffffffffu));
+            if (pending_.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_.notify_all();
+            }
         }
     }
     void loop() {
         uint64_t seen = 0;
-        std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
-            if (stop_) return;
-            seen = gen_;
-            lk.unlock();
-            work();
-            lk.lock();
+            if (!spinUntil([&] { return stop_.load() || (ticket_.load() >> 32) != seen; })) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_.load() || (ticket_.load() >> 32) != seen; });
+            }
+            if (stop_.load()) return;
+            seen = ticket_.load() >> 32;
+            work(seen);
         }
     }
     std::vector<std::thread> th_;
     std::mutex runMu_;  // held by the caller whose job the workers run
     std::mutex mu_;
     std::condition_variable cv_, done_;
-    const std::function<void(int)>* job_ = nullptr;
-    int njobs_ = 0, pending_ = 0;
-    std::atomic<int> next_{0};
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<const std::function<void(int)>*> job_{nullptr};
+    std::atomic<int> njobs_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<uint64_t> ticket_{0};  // generation << 32 | next job index
+    std::atomic<bool> stop_{false};
 };
 
-// Runs f(c, lo, hi) over channels x [0, n) samples: inline below ~1 MiB of data, else split
-// into slices over the pool.
+// Runs f(c, lo, hi) over channels x [0, n) samples: inline below ~1 MiB of data, else split over
+// the pool -- whole channels per job when there are many channels (2 jobs per worker), else
+// slices of channels.
 inline void forSlices(int C, int64_t n, size_t bytesPerSample, const std::function<void(int, int64_t, int64_t)>& f) {
     const size_t total = static_cast<size_t>(C) * static_cast<size_t>(std::max<int64_t>(n, 0)) * bytesPerSample;
     if (total < (size_t(1) << 20)) {
@@ -583,7 +609,14 @@ inline void forSlices(int C, int64_t n, size_t bytesPerSample, const std::functi
         return;
     }
     Pool& pool = Pool::get();
-    const int per = std::max<int>(1, (pool.workers() * 2 + C - 1) / C);  // slices per channel
+    const int J = pool.workers() * 2;
+    if (C >= J) {
+        pool.run(J, [&](int j) {
+            for (int c = static_cast<int>(static_cast<int64_t>(C) * j / J); c < static_cast<int64_t>(C) * (j + 1) / J; ++c) f(c, 0, n);
+        });
+        return;
+    }
+    const int per = std::max<int>(1, (J + C - 1) / C);  // slices per channel
     const int64_t step = (n + per - 1) / per;
     pool.run(C * per, [&](int i) {
         const int c = i / per, k = i - c * per;
@@ -1526,8 +1559,49 @@ int64_t estimate(const Handle* h, int64_t n) {
 
 // Host input -> pinned staging in the compute dtype (f64 -> f32 rounds exactly as the kernels'
 // loads would: the result is bit-identical to handing them the f64 input).
+// Host conversions of the staging copies, AVX2 where the CPU has it.  The output copy into the
+// caller's arrays uses streaming stores (no read-for-ownership of 8.9 MB per 256-channel 4096-frame
+// call); each job ends with an sfence so the stores are globally visible before the pool's hand-off.
+__attribute__((target("avx2"))) void cvtD2F(float* d, const double* s, int64_t n) {
+    int64_t i = 0;
+    for (; i + 8 <= n; i += 8)
+        _mm256_storeu_ps(d + i, _mm256_set_m128(_mm256_cvtpd_ps(_mm256_loadu_pd(s + i + 4)),
+                                                _mm256_cvtpd_ps(_mm256_loadu_pd(s + i))));
+    for (; i < n; ++i) d[i] = static_cast<float>(s[i]);
+}
+__attribute__((target("avx2"))) void cvtF2DStream(double* d, const float* s, int64_t n) {
+    int64_t i = 0;
+    for (; i < n && (reinterpret_cast<uintptr_t>(d + i) & 31); ++i) d[i] = static_cast<double>(s[i]);
+    for (; i + 8 <= n; i += 8) {
+        _mm256_stream_pd(d + i, _mm256_cvtps_pd(_mm_loadu_ps(s + i)));
+        _mm256_stream_pd(d + i + 4, _mm256_cvtps_pd(_mm_loadu_ps(s + i + 4)));
+    }
+    for (; i < n; ++i) d[i] = static_cast<double>(s[i]);
+    _mm_sfence();
+}
+__attribute__((target("avx2"))) void copyD2DStream(double* d, const double* s, int64_t n) {
+    int64_t i = 0;
+    for (; i < n && (reinterpret_cast<uintptr_t>(d + i) & 31); ++i) d[i] = s[i];
+    for (; i + 8 <= n; i += 8) {
+        _mm256_stream_pd(d + i, _mm256_loadu_pd(s + i));
+        _mm256_stream_pd(d + i + 4, _mm256_loadu_pd(s + i + 4));
+    }
+    for (; i < n; ++i) d[i] = s[i];
+    _mm_sfence();
+}
+bool hostAvx2() {
+    static const bool a = __builtin_cpu_supports("avx2");
+    return a;
+}
+
 template <class T>
 void packChannel(void* dst, bool f64, const T* src, int64_t lo, int64_t hi) {
+    if constexpr (std::is_same<T, double>::value) {
+        if (!f64 && hostAvx2()) {
+            cvtD2F(static_cast<float*>(dst) + lo, src + lo, hi - lo);
+            return;
+        }
+    }
     if (f64) {
         double* d = static_cast<double*>(dst);
         for (int64_t i = lo; i < hi; ++i) d[i] = static_cast<double>(src[i]);
@@ -1538,6 +1612,13 @@ void packChannel(void* dst, bool f64, const T* src, int64_t lo, int64_t hi) {
 }
 template <class T>
 void unpackChannel(T* dst, bool f64, const void* src, int64_t lo, int64_t hi) {
+    if constexpr (std::is_same<T, double>::value) {
+        if (hostAvx2() && hi - lo >= 64) {
+            if (f64) copyD2DStream(dst + lo, static_cast<const double*>(src) + lo, hi - lo);
+            else cvtF2DStream(dst + lo, static_cast<const float*>(src) + lo, hi - lo);
+            return;
+        }
+    }
     if (f64) {
         const double* s = static_cast<const double*>(src);
         for (int64_t i = lo; i < hi; ++i) dst[i] = static_cast<T>(s[i]);
@@ -1765,6 +1846,28 @@ gar_status gar_flush_f32(gar_resampler* r, float* out, int64_t cap, int64_t* n_o
     return monoCall<float>(r, 0, nullptr, 0, out, cap, n_out, true, false);
 }
 
+// Development (GAR_HOST_TRACE=1, read once): per-call phase times of the host multi-channel path on
+// stderr (pack into the pinned staging, launches, wait for the device, unpack), microseconds.
+struct HostTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    double ph[4] = {0, 0, 0, 0};
+    HostTrace() : on(enabled()), t0(std::chrono::steady_clock::now()) {}
+    static bool enabled() {
+        static const bool e = [] { const char* v = std::getenv("GAR_HOST_TRACE"); return v && v[0] == '1'; }();
+        return e;
+    }
+    void add(int k) {  // the time since the previous mark belongs to phase k
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        ph[k] += std::chrono::duration<double, std::micro>(t - t0).count();
+        t0 = t;
+    }
+    ~HostTrace() {
+        if (on) fprintf(stderr, "host-trace pack %.1f launch %.1f device-wait %.1f unpack %.1f us\n", ph[0], ph[1], ph[2], ph[3]);
+    }
+};
+
 gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int32_t nch, int64_t n,
                                  double* const* out, int64_t cap, int64_t* n_out) {
     if (!r) return guard(GAR_ERR_INVALID_ARGUMENT, "nil resampler");
@@ -1790,6 +1893,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
         const int64_t ocap = (std::max<int64_t>(need, 1) + 3) / 4 * 4;
         char* hin = nullptr;
         char* hout = nullptr;
+        HostTrace tr;
         if (!h->dry) {
             if (n > 0) {
                 hin = static_cast<char*>(h->hostIn.ensure(static_cast<size_t>(n) * C * es));
@@ -1799,6 +1903,7 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
             }
             hout = static_cast<char*>(h->hostOut.ensure(static_cast<size_t>(ocap) * C * es));
         }
+        tr.add(0);
         std::vector<int64_t> got(h->groups.size());
         for (size_t gi = 0; gi < h->groups.size(); ++gi) {
             Group& g = h->groups[gi];
@@ -1819,13 +1924,16 @@ gar_status gar_process_multi_f64(gar_resampler* r, const double* const* in, int3
             for (int c = g.c0; c < g.c0 + g.C; ++c)
                 if (n_out) n_out[c] = got[gi];
         }
+        tr.add(1);
         if (!h->dry) {
             HIPCHK(hipStreamSynchronize(h->stream));
+            tr.add(2);
             const int64_t gmax = got.empty() ? 0 : *std::max_element(got.begin(), got.end());
             forSlices(C, gmax, es + 8, [&](int c, int64_t lo, int64_t hi) {
                 const int64_t m = got[groupOf(h, c) - h->groups.data()];
                 if (lo < m) unpackChannel<double>(out[c], h->f64, hout + static_cast<size_t>(c) * ocap * es, lo, std::min(hi, m));
             });
+            tr.add(3);
             trimHost(h);
         }
         return GAR_OK;

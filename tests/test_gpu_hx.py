@@ -246,3 +246,48 @@ def test_hxt_expired_wait_is_a_device_error(gar, cuda, monkeypatch):
     again = r.process_device(x).clone()
     r.synchronize()
     assert torch.equal(again, ref)
+
+
+@pytest.mark.parametrize("ch,dtype,mono_first", [(256, "F32", False), (64, "F64", False), (24, "F32", True)])
+def test_large_host_calls_equal_device_stream(gar, cuda, ch, dtype, mono_first):
+    """Host ProcessMulti calls large enough for the packing pool (AVX2 conversions, streaming
+    stores into the caller's arrays, whole channels per job) return exactly the samples and counts
+    of the same streams run through the device API in one call each (chunked == one-shot, stereo ==
+    monos), including a handle whose channel 0 was advanced alone first (two channel groups), and
+    FlushMulti afterwards."""
+    import torch
+    n = 2 * 4096 if ch >= 256 else 6 * 4096 + 77
+    x = signal(n, ch, 44100, seed=ch).astype(np.float32).astype(np.float64)
+    dt = getattr(gar, dtype)
+    tdt = torch.float32 if dtype == "F32" else torch.float64
+    rh = gar.New(gar.Config(44100, 48000, ch, gar.QualityHigh, ComputeDtype=dt))
+    pre = 1000 if mono_first else 0
+    got = [[] for _ in range(ch)]
+    if mono_first:
+        got[0].append(rh.Process(x[:pre, 0]))
+    # channel 0 continues at frame pre, the others start at 0: every call gives all channels k frames
+    lens = [n - pre] if ch >= 256 else [4096 * 5 + 11, n - pre - (4096 * 5 + 11)]
+    s = 0
+    for k in lens:
+        res = rh.ProcessMulti([x[s + (pre if c == 0 else 0):s + (pre if c == 0 else 0) + k, c] for c in range(ch)])
+        for c in range(ch):
+            got[c].append(res[c])
+        s += k
+    tails = rh.FlushMulti()
+    got = [np.concatenate(got[c] + [tails[c]]) for c in range(ch)]
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(tdt).cuda()
+    if mono_first:
+        ref = []
+        for c in range(ch):
+            r1 = gar.New(gar.Config(44100, 48000, 1, gar.QualityHigh, ComputeDtype=dt))
+            L = n if c == 0 else n - pre
+            y = torch.cat([r1.process_device(xd[:L, c:c + 1].contiguous()), r1.flush_device(dtype=tdt)])
+            ref.append(y[:, 0].double().cpu().numpy())
+    else:
+        rd = gar.New(gar.Config(44100, 48000, ch, gar.QualityHigh, ComputeDtype=dt))
+        y = torch.cat([rd.process_device(xd), rd.flush_device(dtype=tdt)]).double().cpu().numpy()
+        ref = [y[:, c] for c in range(ch)]
+    torch.cuda.synchronize()
+    for c in range(ch):
+        assert got[c].shape == ref[c].shape, (c, got[c].shape, ref[c].shape)
+        np.testing.assert_array_equal(got[c], ref[c])
