@@ -67,6 +67,14 @@ __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, T
 //   [W, Wl) are filled with finite data (A is 0 there, but 0*NaN = NaN).
 //   Wave (cg, wt) runs wave programs wt, wt+nwt, ... (gar_plan.hpp BgProg).
 // ---------------------------------------------------------------------------
+// Development build (-DGAR_BG_DEV=1, GAR_BG_PROF=1): s_memtime phase stamps of the small f64
+// launches (bg_rt_kernel / bg_rb_kernel) summed into BgGrid::prof and printed at exit.
+#ifndef GAR_BG_DEV
+#define GAR_BG_DEV 0
+#endif
+constexpr bool kBgDev = GAR_BG_DEV;
+constexpr int kBgProfWords = 64;
+
 struct BgGrid {
     int Pc, Qc, Kc, W, Wl, Ws, G;
     int64_t a_lo;
@@ -81,6 +89,37 @@ struct BgGrid {
     int rbK0[kBgRbKMaxProg];
     void* hdst;       // folded history keep (HistCopy): hdst[(t - ht0) * C + c] = src(t, c), t < ht0 + hn
     int64_t ht0, hn;
+    unsigned long long* prof;  // development stamps (kBgDev), else null
+};
+
+// Development: phase stamps of waves 0 and 1 of a workgroup's first item (words base + 8 wt + k:
+// k = 0..5 phase cycles, 6 count) and the workgroup's life (base + 16: count, life sum, first entry,
+// last exit, last entry; s_memrealtime ticks of 10 ns).
+struct BgStamps {
+    unsigned long long t[7];
+    unsigned long long r0;
+    int k;
+    bool on;
+    __device__ BgStamps(const BgGrid& g, bool first) : k(0), on(kBgDev && g.prof && first && (threadIdx.x & 63) == 0 && threadIdx.x < 128) {
+        if (on) { r0 = __builtin_amdgcn_s_memrealtime(); t[k++] = __builtin_amdgcn_s_memtime(); }
+    }
+    __device__ void mark() { if (kBgDev && on && k < 7) t[k++] = __builtin_amdgcn_s_memtime(); }
+    __device__ void done(const BgGrid& g, int base) {
+        if (!(kBgDev && on)) return;
+        __builtin_amdgcn_s_waitcnt(0);
+        mark();
+        const int wt = threadIdx.x >> 6;
+        for (int i = 1; i < k; ++i) atomicAdd(g.prof + base + 8 * wt + i - 1, t[i] - t[i - 1]);
+        atomicAdd(g.prof + base + 8 * wt + 6, 1ull);
+        if (wt == 0) {
+            const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(g.prof + base + 16, 1ull);
+            atomicAdd(g.prof + base + 17, r1 - r0);
+            atomicMin(g.prof + base + 18, r0);
+            atomicMax(g.prof + base + 19, r1);
+            atomicMax(g.prof + base + 20, r0);
+        }
+    }
 };
 
 // f32 epilogue of one 16x16 accumulator: lane holds rows r0..r0+3 (r0 =
@@ -519,6 +558,7 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
     const TC* Aimg = static_cast<const TC*>(p.A);
+    BgStamps stm(g, keep);
     const int b = v / p.nrb, rb = v - b * p.nrb;
     const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
     const int col = b * 16 + (lane & 15);
@@ -563,6 +603,8 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
             for (int s = 0; s < NS; ++s) B[s] = colOk ? srcRead<TC>(src, t0 + 4 * s, c) : TC(0);
         }
         if (keep) bgRbHistKeepW<TC>(src, g, wg, nwg);  // its round trip beside A / B's
+        stm.mark();  // A / B / history loads issued
+        if (kBgDev && stm.on) { __builtin_amdgcn_s_waitcnt(0); stm.mark(); }  // ... and landed
         // every A / B load issued before the first MFMA: one memory round trip for the program
         // (left alone, the scheduler interleaves load -> wait -> MFMA, NS round trips deep)
         __builtin_amdgcn_sched_barrier(0);
@@ -574,9 +616,11 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
         }
         r = acc0 + acc1;
         if (np > 1) slots[wt][lane] = r;
+        if (kBgDev && stm.on) { __builtin_amdgcn_s_waitcnt(0); stm.mark(); }  // MFMA chain done
     }
     if (np > 1) {
         __syncthreads();
+        stm.mark();  // reduction barrier
         if (wt == 0) {
             V sum = slots[0][lane];
             for (int k = 1; k < np; ++k) sum += slots[k][lane];
@@ -586,6 +630,7 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
     } else if (wt == 0 && !(g.dbg & 2)) {
         storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
     }
+    stm.done(g, 32);
 }
 
 template <class TC, int NS>
@@ -628,6 +673,7 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
     V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(nphys) * sizeof(TC) + 15) / 16 * 16);
     const int nkb = (g.nchunk + 15) / 16;
     const bool same = srcSameType<TC>(src);
+    BgStamps stm(g, keep);
     const int rb = v % p.nrb, cb = v / p.nrb;
     const int c = cb / nkb, kb = cb - c * nkb;
     const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
@@ -656,7 +702,9 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
         }
     }
     if (keep) bgRbHistKeepW<TC>(src, g, wg, nwg);  // its round trip beside the staging
+    stm.mark();  // A issued, window staged by this wave
     __syncthreads();  // window staged
+    stm.mark();
     const int n = lane & 15, kq = lane >> 4;
     const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
     const bool colOk = 16 * kb + n < g.nchunk;
@@ -681,9 +729,11 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
         }
         r = acc0 + acc1;
         if (np > 1) slots[wt * 64 + lane] = r;
+        if (kBgDev && stm.on) { __builtin_amdgcn_s_waitcnt(0); stm.mark(); }  // B reads + MFMA chain done
     }
     if (np > 1) {
         __syncthreads();
+        stm.mark();  // reduction barrier
         if (wt == 0) {
             V sum = slots[lane];
             for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
@@ -693,6 +743,7 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
         storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
     }
     __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
+    stm.done(g, 0);
 }
 
 template <class TC, int NS>

@@ -70,6 +70,37 @@ hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDes
 // Small-launch geometry of a row-block-aligned f64 plan (stream chunks): returns the launch mode
 // (0 not a small launch; 1 bg_rb_kernel, 2 bg_rt_kernel, 3 bg_rc_kernel) with g, the dynamic LDS and
 // the grid filled in.  The history keep hc is taken (hc->done) when the mode is not 0.
+// development: GAR_BG_PROF=1 (with a -DGAR_BG_DEV=1 build of the f64 units) sums the small
+// launches' phase stamps and prints them at exit
+static unsigned long long* bgProfBuf() {
+    static unsigned long long* p = nullptr;
+    static bool init = false;
+    if (!init) {
+        init = true;
+        if (std::getenv("GAR_BG_PROF") && hipMalloc(&p, kBgProfWords * sizeof(unsigned long long)) == hipSuccess) {
+            (void)hipMemset(p, 0, kBgProfWords * sizeof(unsigned long long));
+            (void)hipMemset(p + 18, 0xff, sizeof(unsigned long long));
+            (void)hipMemset(p + 32 + 18, 0xff, sizeof(unsigned long long));
+            std::atexit([] {
+                static unsigned long long h[kBgProfWords] = {};
+                if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, p, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return;
+                const char* names[2] = {"bg_rt", "bg_rb"};
+                for (int k = 0; k < 2; ++k) {
+                    const unsigned long long* q = h + 32 * k;
+                    if (!q[16]) continue;
+                    for (int w = 0; w < 2; ++w) {
+                        const double n = q[8 * w + 6] ? static_cast<double>(q[8 * w + 6]) : 1;
+                        fprintf(stderr, "%s wave %d phases (cycles): %.0f %.0f %.0f %.0f %.0f %.0f (n %llu)\n", names[k], w, q[8 * w] / n,
+                                q[8 * w + 1] / n, q[8 * w + 2] / n, q[8 * w + 3] / n, q[8 * w + 4] / n, q[8 * w + 5] / n, q[8 * w + 6]);
+                    }
+                    fprintf(stderr, "%s workgroups %llu: life %.2f us avg\n", names[k], q[16], q[17] / static_cast<double>(q[16]) / 100.0);
+                }
+            });
+        }
+    }
+    return p;
+}
+
 static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, int ncu, BgGrid& g, size_t& lds,
                        int64_t& blocks) {
     static const int knobDbg = std::getenv("GAR_BG_DBG") ? std::atoi(std::getenv("GAR_BG_DBG")) : 0;
@@ -104,6 +135,7 @@ static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, i
     g.parity = 0;
     g.hdst = nullptr;
     g.ht0 = g.hn = 0;
+    g.prof = kBgDev ? bgProfBuf() : nullptr;
     if (hc && hc->n > 0 && hc->dst) {
         g.hdst = hc->dst;
         g.ht0 = hc->t0;
@@ -255,6 +287,7 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     if (g.nblocks <= 0) return hipSuccess;
     int64_t blocks = std::min<int64_t>(g.nblocks, static_cast<int64_t>(ncu) * (knobWgPerCu > 0 ? knobWgPerCu : 2));
     g.hdst = nullptr;
+    g.prof = nullptr;
     g.ht0 = g.hn = 0;
     if (hc && hc->n > 0 && hc->dst) {  // history keep folded into this launch (no gather_kernel after it)
         g.hdst = hc->dst;
