@@ -348,7 +348,7 @@ def pmc_traffic(args, workload, kernel_keys):
 
 
 # bytes per lane of the dominant kernel's input loads (gar_hxs.hpp hxsRegIssue / gar_hxt.hpp hxtIssue:
-# STEREO buffer_load_dwordx2, ROW16 dwordx4, PCM16 stereo dword; cfg5's bg_rb_kernel: one 8-B f64
+# STEREO buffer_load_dwordx2, ROW16 dwordx4, PCM16 stereo dword; cfg5's bg_rt / bg_rb kernels: one 8-B f64
 # global load per lane and step for A and B (gar_bg.hpp bg_rb_kernel), each lane of a B load on its
 # own 64-B row of the interleaved 8-channel stream -- the x2 streaming calibration is an upper bound
 # there, so bench also reports the uncorrected read bytes)
@@ -651,11 +651,15 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
                 "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
         paired = dom == 0 and not prof[2][1] and sidx > 0 and geoms[sidx - 1][1].kind == 3
-        kernel_keys = ["poly_kernel"] if dom == 4 else ["bg_kernel", "bg_rb_kernel", "bg_pair_kernel"]
         chunked = bool(w["chunk"])
+        # the kernel that runs the dominant kind: small launches of a chunked stream run the decimator
+        # (<= 2 row blocks) on bg_rt_kernel and the composite on bg_rb_kernel (gar_kernels.hip
+        # bgSmallGrid); one-shot streams run bg_kernel
+        small = ("bg_rt_kernel" if dom == 2 else "bg_pair_kernel" if paired else "bg_rb_kernel")
+        kernel_keys = (["poly_kernel"] if dom == 4 else [small] if chunked else ["bg_kernel"])
         kern = ('poly_kernel<double>' if dom == 4 else
-                ('bg_pair_kernel<double> (decimator items + ' if paired else '') +
-                ('bg_rb_kernel<double>' if chunked else 'bg_kernel<double>'))
+                ('bg_pair_kernel<double> (decimator items + bg_rb_kernel<double>' if paired else
+                 f'{small}<double>' if chunked else 'bg_kernel<double>'))
         kname = (f"{kern} ({KIND_NAMES[dom]}, stage {sidx}: {48000:g}->{48000 * st_ratio:g} Hz engine"
                  f"{', with the decimator stage before it in the same launch)' if paired else ''}, v_mfma_f64_16x16x4_f64)")
         # a pair launch reads the decimator's input (the stream) and writes the composite's output
