@@ -25,7 +25,11 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 PIN_DB = 0.05            # oracle vs a published float64 Go number (exact restatement: observed <= 0.01)
 F32_PIN_DB = 1.0         # float32: the SIMD summation order of tphakala/simd is not known
 GPU_F64_DB = 0.05        # HIP float64 vs oracle float64
-GPU_F32_SLACK_DB = 3.0   # HIP float32 may not be worse than the reference's own float32 engine by more
+# HIP float32 may not be worse than the reference's own float32 engine by more.  Measured margins
+# (tools/f32_thd_margin.py, every GPU_CASES row; deterministic bits, so the same on every box): split-f16
+# F32 -6.02 .. +1.19 dB, exact F32 -7.68 .. +1.74 dB -- summation-order noise at the float32 floor
+# (-130 .. -156 dB THD); round 4 allowed 3 dB
+GPU_F32_SLACK_DB = 2.0
 GPU_SNR_DB = 0.1
 GPU_RIPPLE_DB = 0.01
 
@@ -133,7 +137,7 @@ def test_gpu_f64_quality_equals_oracle(gar, O, cuda, ir, orr, name):
 @pytest.mark.parametrize("ir,orr,name", GPU_CASES, ids=_ids(GPU_CASES))
 def test_gpu_f32_quality(gar, O, cuda, ir, orr, name, dtype):
     """float32 compute (split-f16 MFMA / exact-f32 MFMA) vs the reference's own float32
-    engine (Resampler[float32]): THD no more than 3 dB worse, same SNR."""
+    engine (Resampler[float32]): THD no more than GPU_F32_SLACK_DB (2 dB) worse, same SNR."""
     q = Q.ENGINE_Q[name]
     g, o32 = _gpu_run(gar, ir, orr, q, getattr(gar, dtype)), _oracle_run(O, ir, orr, q, f32=True)
     assert Q.thd_internal(g, ir, orr) <= Q.thd_internal(o32, ir, orr) + GPU_F32_SLACK_DB
@@ -180,8 +184,8 @@ def _oracle_new_chain_f32(O, ir, orr, preset_name, x):
 @pytest.mark.parametrize("dtype", ["F32", "F64"])
 def test_gpu_new_path_thd(gar, O, cuda, preset, ir, orr, dtype):
     """The BASELINE New path (Quality24Bit / Quality32Bit designs, float32 I/O): THD of the
-    HIP output within 0.05 dB of the float64 oracle (F64 compute), or no more than 3 dB
-    worse than the same stage chain on the reference's float32 engine (F32 compute)."""
+    HIP output within 0.05 dB of the float64 oracle (F64 compute), or no more than
+    GPU_F32_SLACK_DB worse than the same stage chain on the reference's float32 engine (F32 compute)."""
     x = Q.sine_input(ir)
     r = gar.New(gar.Config(ir, orr, 1, getattr(gar, "Quality" + preset), ComputeDtype=getattr(gar, dtype)))
     y = np.concatenate([r.ProcessFloat32(x.astype(np.float32)), r.Flush()]).astype(np.float64)
