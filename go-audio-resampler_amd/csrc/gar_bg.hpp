@@ -633,14 +633,33 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
     stm.done(g, 32);
 }
 
+// XCD-grouped item order of the small launches: workgroup slot bb runs item (group, member) with
+// group = 8 (bb / 8 / M) + bb % 8 and member = (bb / 8) % M, so the M items that read the same
+// input lines (the row blocks of one column block; the row blocks x channels of one time block) run
+// on workgroup slots of one residue mod 8, i.e. on one XCD under the round-robin dispatch, and share
+// its L2 (cfg5 decimator: each 64-B line of the 8-channel stream was fetched by 8 XCDs).  The grid
+// is 8 M ceil(ngroups / 8) slots (a multiple of 8 also when capped); slots past the last group idle.
+__host__ __device__ inline int64_t bgXcdSlots(int64_t ngroups, int64_t M) { return 8 * M * ((ngroups + 7) / 8); }
+__device__ __forceinline__ bool bgXcdItem(int64_t bb, int M, int ngroups, int& group, int& member) {
+    const int64_t rest = bb >> 3;
+    member = static_cast<int>(rest % M);
+    group = static_cast<int>((rest / M) * 8 + (bb & 7));
+    return group < ngroups;
+}
+
 template <class TC, int NS>
 __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
     typedef typename Acc<TC>::V V;
     __shared__ V slots[kBgRbMaxWaves][64];
-    const int nv = g.nblocks * p.nrb;
-    for (int v = blockIdx.x; v < nv; v += gridDim.x)  // uniform per workgroup
-        bgRbItem<TC, NS>(p, src, od, g, v, slots, v == static_cast<int>(blockIdx.x), blockIdx.x, gridDim.x);
-    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);  // a workgroup without an item
+    const int64_t total = bgXcdSlots(g.nblocks, p.nrb);
+    bool kept = false;
+    for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {  // uniform per workgroup
+        int b, rb;
+        if (!bgXcdItem(bb, p.nrb, g.nblocks, b, rb)) continue;
+        bgRbItem<TC, NS>(p, src, od, g, b * p.nrb + rb, slots, !kept, blockIdx.x, gridDim.x);
+        kept = true;
+    }
+    if (!kept) bgRbHistKeep<TC>(src, g);  // a workgroup without an item
 }
 
 // Small launches of row-block-aligned plans, time-major (default; bg_rb_kernel is the GAR_BG_RT=0
@@ -750,12 +769,19 @@ template <class TC, int NS>
 __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nkb = (g.nchunk + 15) / 16;
-    const int nv = p.nrb * g.C * nkb;
-    for (int v = blockIdx.x; v < nv; v += gridDim.x)  // uniform per workgroup
-        bgRtItem<TC, NS>(p, src, od, g, v, smem, v == static_cast<int>(blockIdx.x), blockIdx.x, gridDim.x);
-    // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
-    // no second pass); a workgroup without one copies it here
-    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
+    const int M = p.nrb * g.C;  // items of one time block: row blocks x channels
+    const int64_t total = bgXcdSlots(nkb, M);
+    bool kept = false;
+    for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {  // uniform per workgroup
+        int kb, m;
+        if (!bgXcdItem(bb, M, nkb, kb, m)) continue;
+        const int rb = m % p.nrb, c = m / p.nrb;
+        bgRtItem<TC, NS>(p, src, od, g, rb + p.nrb * (c * nkb + kb), smem, !kept, blockIdx.x, gridDim.x);
+        kept = true;
+    }
+    // every thread of a workgroup with an item copied its share in its first item (no
+    // second pass); a workgroup without one copies it here
+    if (!kept) bgRbHistKeep<TC>(src, g);
 }
 
 // Small launches of row-block-aligned plans, column blocks as bg_rb_kernel (16 consecutive columns,

@@ -337,8 +337,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.err = od.err;
     x.pollMax = 1 << 24;
     x.faultNeed = 0;
-    static const int knobCoop = std::getenv("GAR_HXT_COOP") ? std::atoi(std::getenv("GAR_HXT_COOP")) : 1;
-    x.coop = knobCoop;
+    static const int knobCoop = std::getenv("GAR_HXT_COOP") ? std::atoi(std::getenv("GAR_HXT_COOP")) : 2;
+    x.coop = std::max(0, std::min(2, knobCoop));
     if (hxt) {
         const char* f = std::getenv("GAR_HXT_FAULT");
         if (f && f[0] == '1') {

@@ -366,7 +366,10 @@ __device__ __forceinline__ bool hxtStage0Fast(const HxsArgs& x, int b) {
 // ~45k cycles, 15 % of a cfg2 workgroup's life).  Items as the loaders' (FMT 1: quad + 64-row piece,
 // two chunks of stereo frames; FMT 2: 16-row piece, lane = 16 quad + row), kCoopB in flight per
 // wave, each staged through hxsPutItem (split, mirror, loud marking) like the edge gathers.
-template <int FMT>
+// Ordered variant (knob GAR_HXT_COOP=2): the compute waves meet the loaders at a first barrier right
+// after issuing their first batch; the loaders issue load P only after it and load P + 1 only after the
+// window is complete, so the chip's first windows are not queued behind the loaders' loads.
+template <int FMT, int kCoopB, bool kOrdered>
 __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared& sh, int b, int w, int nw, int lane) {
     const HxsArgsP xp = hxsCold();
     const HxsRegSrc rs = hxsRegSrc<FMT>(xp, b, lane);
@@ -376,7 +379,7 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
     st.fast = true;
     const int Wg = x.Wg;
     const int nit = FMT == 1 ? 4 * ((Wg + 63) >> 6) : (Wg + 15) >> 4;
-    constexpr int kCoopB = 4;
+    bool met = !kOrdered;
     for (int it0 = w; it0 < nit; it0 += kCoopB * nw) {
         f32x4 e[kCoopB];
 #pragma unroll
@@ -395,6 +398,10 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
                 e[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
             }
         }
+        if (!met) {  // first batch issued: let the loaders issue theirs
+            hxsBarrier();
+            met = true;
+        }
 #pragma unroll
         for (int u = 0; u < kCoopB; ++u) {
             const int it = it0 + u * nw;
@@ -404,11 +411,12 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
             if (row < Wg) hxsPutItem(xp, st, 0, q, row, e[u], sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
         }
     }
+    if (!met) hxsBarrier();  // a wave without items still meets the loaders
 }
 
 template <int FMT, int NL>
 __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh, const HxtSync& sy, int b, int l,
-                                           int lane, bool coop, unsigned long long* waited) {
+                                           int lane, int coop, unsigned long long* waited) {
     if constexpr (GAR_HXT_LPRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXT_LPRIO);
     const HxsArgsP xp = hxsCold();
     const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
@@ -434,9 +442,18 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     // with the cooperative fill the compute waves stage loads 0 .. P-1: the loaders start at P, with
     // its loads in flight across the fill's barrier
     const int jStart = coop ? P : 0;
+    if (coop == 2) {
+        // ordered fill: load P after the compute waves' first window batch, load P + 1 after the window
+        hxsBarrier();
+        fastL[0] = hxtIssue<FMT, NL>(stage(jStart), jStart < nL, rs, l, buf[0]);
+        hxsBarrier();  // the first window is in the ring
 #pragma unroll
-    for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(jStart + d), jStart + d < nL, rs, l, buf[d]);
-    if (coop) hxsBarrier();  // the first window is in the ring (no vector-memory wait: the loads stay in flight)
+        for (int d = 1; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(jStart + d), jStart + d < nL, rs, l, buf[d]);
+    } else {
+#pragma unroll
+        for (int d = 0; d < kHxtD; ++d) fastL[d] = hxtIssue<FMT, NL>(stage(jStart + d), jStart + d < nL, rs, l, buf[d]);
+        if (coop) hxsBarrier();  // the first window is in the ring (no vector-memory wait: the loads stay in flight)
+    }
     // ring row of load j's first row (incremental: T0 % R) and the groups its rows' previous
     // occupants belong to (hxtFreeNeed, incremental)
     int p0 = coop ? Wg : 0, last = Wg + GQ - 1 - R, need = 0;
@@ -576,7 +593,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
 
 template <int NS, int VST, int FMT>
 __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int b, int wt,
-                                           int lane, int nl, bool coop, unsigned long long* st) {
+                                           int lane, int nl, int coop, unsigned long long* st) {
     // A of the wave's row block (kept in registers only inside this role: the loaders' registers
     // are the load buffers)
     const HxtRole ro = hxtRole(x, wt);
@@ -590,7 +607,8 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
     }
     if (kHxsDev && st) st[6] = __builtin_amdgcn_s_memtime();
     if (coop) {  // the block's first window, staged by every compute wave (A lands meanwhile)
-        hxtCoopStage0<FMT>(x, sh_, b, wt, x.ncomp, lane);
+        if (coop == 2) hxtCoopStage0<FMT, 4, true>(x, sh_, b, wt, x.ncomp, lane);
+        else hxtCoopStage0<FMT, 4, false>(x, sh_, b, wt, x.ncomp, lane);
         hxsBarrier();
     }
     if (kHxsDev && st) st[7] = __builtin_amdgcn_s_memtime();
@@ -653,9 +671,10 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
             s.loudLo[threadIdx.x] = INT_MAX;
             s.loudHi[threadIdx.x] = -1;
         }
-        // cooperative fill (knob x.coop): loads 0 .. P-1 complete once the fill's barrier passes
+        // cooperative fill (knob x.coop, GAR_HXT_COOP: 2 ordered (default), 1 unordered, 0 off): loads
+        // 0 .. P-1 complete once the fill's barrier passes
         const int GQb = x.G * x.Qc, Pb = (x.Wg + GQb - 1) / GQb;
-        const bool coop = x.coop && hxtStage0Fast(x, b);
+        const int coop = hxtStage0Fast(x, b) ? x.coop : 0;  // 0 loaders stage the first window, 1 / 2 the compute waves
         if (threadIdx.x < 2 * kHxtSlots) sy.ldArr[threadIdx.x] = (coop && static_cast<int>(threadIdx.x) < Pb) ? NL : 0;  // arrival slots
         if (threadIdx.x == 64) *s.flag = 0;
         __syncthreads();

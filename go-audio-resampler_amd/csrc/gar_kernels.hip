@@ -152,7 +152,7 @@ static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, i
     if ((knobRt == 1 || (knobRt < 0 && p.nrb <= 2)) && rtLds <= 64 * 1024) {
         g.rbMode = 2;
         const int64_t nkb = (nmac + 15) / 16;
-        blocks = std::min<int64_t>(nkb * C * p.nrb, 65535);
+        blocks = std::min<int64_t>(bgXcdSlots(nkb, static_cast<int64_t>(C) * p.nrb), 65528);  // XCD-grouped slots
         lds = rtLds;
         return 2;
     }
@@ -163,7 +163,7 @@ static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, i
         lds = rcLds;
         return 3;
     }
-    blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
+    blocks = std::min<int64_t>(bgXcdSlots(g.nblocks, p.nrb), 65528);  // XCD-grouped slots
     lds = 0;
     return 1;
 }
@@ -197,7 +197,9 @@ hipError_t launchBgPair(const BgDev& p0, const SrcDesc& s0, const OutDesc& o0, H
     if (bgSmallGrid(p1, o1, C, &t1, ncu, a.g1, lds1, b1) != 1) return hipErrorNotSupported;  // composite: bg_rb items
     const int64_t n0 = (a.g0.nchunk + 15) / 16 * static_cast<int64_t>(C) * p0.nrb;
     const int64_t n1 = static_cast<int64_t>(a.g1.nblocks) * p1.nrb;
-    if (n0 != b0 || n1 != b1 || n0 + n1 > 65535) return hipErrorNotSupported;  // one item per workgroup
+    (void)b0;
+    (void)b1;
+    if (n0 + n1 > 65535) return hipErrorNotSupported;  // one item per workgroup
     a.p0 = p0; a.p1 = p1;
     a.s0 = s0; a.s1 = s1;
     a.o0 = o0; a.o1 = o1;
