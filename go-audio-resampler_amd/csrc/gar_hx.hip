@@ -87,6 +87,10 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
         const int64_t inEnd = std::min(src.in_base + src.in_len, src.valid_end);
         k0 = std::max<int64_t>({0, ceilDiv(od.o_lo - a_lo * Pc, GP), ceilDiv(src.in_base - a_lo * Qc, GQ)});
         k1 = std::min<int64_t>({nchunk, floorDiv(od.o_hi - a_lo * Pc, GP), floorDiv(inEnd - W - a_lo * Qc, GQ) + 1});
+        // an empty interior range stays inside [0, nchunk]: a short call whose windows all cross the
+        // history seam has k0 > nchunk (e.g. 399 frames after 912 history rows), and an interior
+        // range placed past the last chunk made ib1 > nblocks below (sweep: 88.2k -> 44.1k High)
+        k0 = std::min(k0, nchunk);
         if (k1 < k0) k1 = k0;
     }
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
@@ -164,7 +168,7 @@ hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& od, int C
 
     // interior blocks: every column an interior chunk
     x.ib0 = static_cast<int>(std::min<int64_t>((k0 * C + 15) / 16, x.nblocks));
-    x.ib1 = static_cast<int>(std::max<int64_t>(x.ib0, (k1 * C) / 16));
+    x.ib1 = static_cast<int>(std::max<int64_t>(x.ib0, std::min<int64_t>((k1 * C) / 16, x.nblocks)));
     x.fix = p.fix;
     x.fixCap = p.fixCap;
 
