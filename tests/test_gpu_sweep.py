@@ -7,6 +7,8 @@ checks every sample and every count against the CPU oracle, the same tolerances 
 test_gpu_parity.py (BASELINE north_star: float64 <= 1e-12 RMS, float32 <= 1e-6 RMS).  The draw is
 fixed (seed), so a failure names a reproducible case.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -18,7 +20,10 @@ RATES = [8000, 11025, 16000, 22050, 24000, 32000, 37800, 44100, 48000, 64000, 88
 PRESETS = ["QualityQuick", "QualityLow", "QualityMedium", "QualityHigh", "QualityVeryHigh"]
 
 
-def _cases(n=96, seed=20261018):
+CHANNELS = [1, 2, 3, 4, 5, 8, 16, 32]  # 16 / 32: the 16-channel-row kernels
+
+
+def _cases(n=200, seed=20261018):
     rng = np.random.default_rng(seed)
     out = []
     while len(out) < n:
@@ -26,15 +31,16 @@ def _cases(n=96, seed=20261018):
         if ir == orr:
             continue
         preset = PRESETS[int(rng.integers(len(PRESETS)))]
-        ch = int(rng.integers(1, 5))
-        frames = int(rng.integers(3000, 16000))
+        ch = CHANNELS[int(rng.integers(len(CHANNELS)))]
+        frames = int(rng.integers(3000, 16000 if ch <= 8 else 6000))
         chunk = [None, 4096, 777, int(rng.integers(100, 3000))][int(rng.integers(4))]
         dtype = "F64" if preset == "QualityQuick" or rng.random() < 0.5 else "F32"
         out.append((ir, orr, preset, ch, frames, chunk, dtype))
     return out
 
 
-CASES = _cases()
+# GAR_SWEEP_SEED draws another fixed set (exploration); the committed default is the one CI runs
+CASES = _cases(seed=int(os.environ.get("GAR_SWEEP_SEED", "20261018")))
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{f}-{k}-{d}" for a, b, p, c, f, k, d in CASES])
@@ -62,7 +68,7 @@ def test_new_path_sweep_vs_oracle(gar, O, cuda, case):
         assert err <= tol, (c, err)
 
 
-HOST_CASES = _cases(24, seed=77)
+HOST_CASES = _cases(48, seed=int(os.environ.get("GAR_SWEEP_SEED", "77")))
 
 
 @pytest.mark.parametrize("case", HOST_CASES, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{f}-{k}-{d}" for a, b, p, c, f, k, d in HOST_CASES])
