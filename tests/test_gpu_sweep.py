@@ -118,3 +118,74 @@ def test_short_call_after_long_history_f32_decimator(gar, O, cuda):
     for c in range(2):
         assert got.shape[0] == len(want[c])
         assert rms(got[:, c], want[c]) <= F32_RMS_TOL
+
+
+def _odd_cases(n=60, seed=31337):
+    """Arbitrary integer rates (not from the usual families): ratios with fractional polyphase
+    steps (poly_kernel, live cubic coefficients), long rational periods and the Quick cubic stage."""
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = int(rng.integers(8000, 192001)), int(rng.integers(8000, 192001))
+        if ir == orr:
+            continue
+        preset = PRESETS[int(rng.integers(len(PRESETS)))]
+        ch = [1, 2, 3][int(rng.integers(3))]
+        frames = int(rng.integers(2000, 9000))
+        chunk = [None, 4096, 1000][int(rng.integers(3))]
+        dtype = "F64" if preset == "QualityQuick" or rng.random() < 0.5 else "F32"
+        out.append((ir, orr, preset, ch, frames, chunk, dtype))
+    return out
+
+
+ODD_CASES = _odd_cases()
+
+
+@pytest.mark.parametrize("case", ODD_CASES, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{f}-{k}-{d}" for a, b, p, c, f, k, d in ODD_CASES])
+def test_odd_rates_sweep_vs_oracle(gar, O, cuda, case):
+    test_new_path_sweep_vs_oracle(gar, O, cuda, case)
+
+
+def _ragged_cases(n=60, seed=4711):
+    """Calls of random lengths (0, 1, a few frames, hundreds, thousands) in one stream: every small-launch
+    kernel (hxq / hxs_small / bg_rt / bg_rb / edge blocks) and the history seam at every offset."""
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        preset = PRESETS[1 + int(rng.integers(len(PRESETS) - 1))]
+        ch = CHANNELS[int(rng.integers(len(CHANNELS) - 2))]
+        sizes = [int(v) for v in rng.choice([0, 1, 2, 7, 31, 64, 129, 500, 1023, 2048, 4800], size=int(rng.integers(4, 12)))]
+        dtype = "F64" if rng.random() < 0.5 else "F32"
+        out.append((ir, orr, preset, ch, sizes, dtype))
+    return out
+
+
+RAGGED = _ragged_cases()
+
+
+@pytest.mark.parametrize("case", RAGGED, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{len(z)}calls-{d}" for a, b, p, c, z, d in RAGGED])
+def test_ragged_calls_sweep_vs_oracle(gar, O, cuda, case):
+    import torch
+    ir, orr, preset, ch, sizes, dtype = case
+    frames = sum(sizes)
+    x = signal(max(frames, 1), ch, ir, seed=ir + 7 * orr + ch)[:frames]
+    if dtype == "F32":
+        x = x.astype(np.float32).astype(np.float64)
+    tdt = torch.float32 if dtype == "F32" else torch.float64
+    r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=getattr(gar, dtype)))
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(tdt).cuda()
+    parts, s = [], 0
+    for n in sizes:
+        parts.append(r.process_device(xd[s:s + n]).clone())
+        s += n
+    parts.append(r.flush_device(dtype=tdt).clone())
+    torch.cuda.synchronize()
+    got = torch.cat(parts).double().cpu().numpy()
+    want = oracle_new(O, ir, orr, x, getattr(O, "P_" + preset[7:].upper()), chunks=[n for n in sizes])
+    tol = F64_RMS_TOL if dtype == "F64" else F32_RMS_TOL
+    for c in range(ch):
+        assert got.shape[0] == len(want[c]), (c, got.shape, len(want[c]))
+        assert rms(got[:, c], want[c]) <= tol
