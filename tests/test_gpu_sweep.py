@@ -189,3 +189,60 @@ def test_ragged_calls_sweep_vs_oracle(gar, O, cuda, case):
     for c in range(ch):
         assert got.shape[0] == len(want[c]), (c, got.shape, len(want[c]))
         assert rms(got[:, c], want[c]) <= tol
+
+
+def _pcm_cases(n=40, seed=1616):
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        preset = PRESETS[1 + int(rng.integers(len(PRESETS) - 1))]
+        ch = [1, 2, 2, 4][int(rng.integers(4))]
+        bits = [16, 24, 32][int(rng.integers(3))]
+        chunk = [None, 4096, 777][int(rng.integers(3))]
+        dtype = "F64" if rng.random() < 0.5 else "F32"
+        out.append((ir, orr, preset, ch, bits, chunk, dtype))
+    return out
+
+
+PCM = _pcm_cases()
+PCM_MAX = {16: 32767.0, 24: 8388607.0, 32: 2147483647.0}
+
+
+@pytest.mark.parametrize("case", PCM, ids=[f"{a}-{b}-{p[7:]}-{c}ch-pcm{t}-{k}-{d}" for a, b, p, c, t, k, d in PCM])
+def test_pcm_io_sweep_vs_oracle(gar, O, cuda, case):
+    """Integer PCM in and out (cmd/resample-wav/main.go:444-543): the device output against the oracle
+    fed float64(i) / maxVal, converted int(clamp(y, -1, 1) * maxVal).  F64 compute: within 1 LSB, off by
+    one on at most 2 % of the samples (float64 rounding moves a truncation across an integer).  F32
+    compute: the float32 error scaled to the integer range -- RMS <= max(0.15 LSB, F32_RMS_TOL * maxVal)
+    and every sample within 1 + 2e-6 * maxVal LSB (measured up to 1,654 LSB at 32 bits, 8 at 24, 2 at 16)."""
+    import torch
+    ir, orr, preset, ch, bits, chunk, dtype = case
+    frames = 6000
+    mv = PCM_MAX[bits]
+    pcm = np.round(np.clip(signal(frames, ch, ir, seed=ir + orr + bits), -1, 1) * mv * 0.98)
+    pcm = pcm.astype(np.int16 if bits == 16 else np.int32)
+    r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=getattr(gar, dtype)))
+    xd = torch.from_numpy(np.ascontiguousarray(pcm)).cuda()
+    parts, s = [], 0
+    for n in (chunk_sizes(frames, chunk) if chunk else [frames]):
+        parts.append(r.process_device(xd[s:s + n], pcm_bits=bits).clone())
+        s += n
+    parts.append(r.flush_device(dtype=xd.dtype, pcm_bits=bits).clone())
+    torch.cuda.synchronize()
+    got = torch.cat(parts).cpu().numpy().astype(np.int64)
+    want = oracle_new(O, ir, orr, pcm.astype(np.float64) * (1.0 / mv), getattr(O, "P_" + preset[7:].upper()))
+    for c in range(ch):
+        w = np.trunc(np.clip(want[c], -1.0, 1.0) * mv).astype(np.int64)
+        assert got.shape[0] == len(w)
+        d = np.abs(got[:, c] - w)
+        if dtype == "F64":
+            assert d.max(initial=0) <= 1, (c, int(d.max()))
+            assert np.count_nonzero(d) <= 0.02 * max(len(w), 1), (c, int(np.count_nonzero(d)))
+        else:
+            assert d.max(initial=0) <= 1 + 2e-6 * mv, (c, int(d.max()))
+            # RMS in LSB: the float32 error (F32_RMS_TOL of full scale) or, at 16 bits where that is
+            # below one LSB, truncations moved by one on at most ~2 % of the samples
+            assert float(np.sqrt(np.mean(d.astype(np.float64) ** 2))) <= max(0.15, F32_RMS_TOL * mv), c
