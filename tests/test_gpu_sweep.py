@@ -246,3 +246,67 @@ def test_pcm_io_sweep_vs_oracle(gar, O, cuda, case):
             # RMS in LSB: the float32 error (F32_RMS_TOL of full scale) or, at 16 bits where that is
             # below one LSB, truncations moved by one on at most ~2 % of the samples
             assert float(np.sqrt(np.mean(d.astype(np.float64) ** 2))) <= max(0.15, F32_RMS_TOL * mv), c
+
+
+def _layout_cases(n=40, seed=5150):
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        preset = PRESETS[1 + int(rng.integers(len(PRESETS) - 1))]
+        ch = [1, 2, 3, 4, 16][int(rng.integers(5))]
+        lin = ["planar", "padded", "offset"][int(rng.integers(3))]
+        lout = ["inter", "planar", "padded"][int(rng.integers(3))]
+        chunk = [None, 4096, 777][int(rng.integers(3))]
+        dtype = ["F32", "F64"][int(rng.integers(2))]
+        out.append((ir, orr, preset, ch, lin, lout, chunk, dtype))
+    return out
+
+
+LAYOUTS = _layout_cases()
+
+
+def _view(torch, x, layout, dt):
+    """A device view of host array x [frames][ch] in the given memory layout."""
+    n, ch = x.shape
+    if layout == "planar":
+        return torch.from_numpy(np.ascontiguousarray(x.T)).to(dt).cuda().t()
+    if layout == "padded":
+        buf = torch.zeros((n, ch + 3), dtype=dt, device="cuda")
+        buf[:, :ch] = torch.from_numpy(x).to(dt).cuda()
+        return buf[:, :ch]
+    if layout == "offset":
+        flat = torch.zeros(1 + n * ch, dtype=dt, device="cuda")
+        flat[1:] = torch.from_numpy(np.ascontiguousarray(x).reshape(-1)).to(dt).cuda()
+        return flat[1:].view(n, ch)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dt).cuda()
+
+
+@pytest.mark.parametrize("case", LAYOUTS, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{i}-{o}-{k}-{d}" for a, b, p, c, i, o, k, d in LAYOUTS])
+def test_layout_sweep_bits_equal_interleaved(gar, cuda, case):
+    """Any input / output strides give the interleaved layout's bits (gar_process_device takes frame
+    and channel strides; the fast loads are written for interleaved rows, the rest is gathered)."""
+    import torch
+    ir, orr, preset, ch, lin, lout, chunk, dtype = case
+    frames = 7000
+    x = signal(frames, ch, ir, seed=ir + orr + 5 * ch)
+    dt = torch.float32 if dtype == "F32" else torch.float64
+
+    def stream(xv, out_layout):
+        r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=getattr(gar, dtype)))
+        cap = int(frames * orr / ir) + 4096
+        ybuf = _view(torch, np.zeros((cap, ch)), out_layout, dt)
+        o, s = 0, 0
+        for n in (chunk_sizes(frames, chunk) if chunk else [frames]):
+            o += r.process_device(xv[s:s + n], out=ybuf[o:]).shape[0]
+            s += n
+        o += r.flush_device(out=ybuf[o:]).shape[0]
+        torch.cuda.synchronize()
+        return ybuf[:o].double().cpu().numpy()
+
+    want = stream(_view(torch, x, "inter", dt), "inter")
+    got = stream(_view(torch, x, lin, dt), lout)
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)
