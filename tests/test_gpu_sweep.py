@@ -310,3 +310,47 @@ def test_layout_sweep_bits_equal_interleaved(gar, cuda, case):
     got = stream(_view(torch, x, lin, dt), lout)
     assert got.shape == want.shape
     assert np.array_equal(got, want)
+
+
+def _engine_cases(n=40, seed=8080):
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        q = int(rng.integers(10))  # engine.Quality: Quick .. VeryHigh, 16 .. 32 bit (GAR_ENGINE_*)
+        chunk = [None, 4096, 500][int(rng.integers(3))]
+        dtype = "F64" if q == 0 or rng.random() < 0.5 else "F32"
+        out.append((ir, orr, q, chunk, dtype))
+    return out
+
+
+ENGINES = _engine_cases()
+
+
+@pytest.mark.parametrize("case", ENGINES, ids=[f"{a}-{b}-q{q}-{k}-{d}" for a, b, q, k, d in ENGINES])
+def test_engine_seam_sweep_vs_oracle(gar, O, cuda, case):
+    """engine.NewResampler[F](in, out, engine.Quality) (internal/engine/resampler.go:51-179, the seam
+    cmd/resample-wav drives) through gar_new_engine_quality: host Process / ProcessFloat32 + Flush
+    against the oracle's engine (float64; the F32 handle against the float64 engine at the float32
+    tolerance)."""
+    ir, orr, q, chunk, dtype = case
+    frames = 9000
+    x = signal(frames, 1, ir, seed=ir + 3 * orr + q)[:, 0]
+    if dtype == "F32":
+        x = x.astype(np.float32).astype(np.float64)
+    r = gar.EngineNewResampler(ir, orr, q, getattr(gar, dtype))
+    e = O.Engine(ir, orr, q)
+    parts, want, s = [], [], 0
+    for n in (chunk_sizes(frames, chunk) if chunk else [frames]):
+        seg = x[s:s + n]
+        parts.append(r.Process(seg) if dtype == "F64" else r.ProcessFloat32(seg.astype(np.float32)))
+        want.append(e.process(seg))
+        s += n
+    parts.append(r.Flush())
+    want.append(e.flush())
+    got = np.concatenate(parts).astype(np.float64)
+    want = np.concatenate(want)
+    assert got.shape == want.shape
+    assert rms(got, want) <= (F64_RMS_TOL if dtype == "F64" else F32_RMS_TOL)
