@@ -354,3 +354,50 @@ def test_engine_seam_sweep_vs_oracle(gar, O, cuda, case):
     want = np.concatenate(want)
     assert got.shape == want.shape
     assert rms(got, want) <= (F64_RMS_TOL if dtype == "F64" else F32_RMS_TOL)
+
+
+def _batch_cases(n=24, seed=2424):
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        preset = PRESETS[1 + int(rng.integers(len(PRESETS) - 1))]
+        streams = [1, 3, 7, 16, 64][int(rng.integers(5))]
+        ch = [1, 2][int(rng.integers(2))]
+        chunk = [None, 4096, 999][int(rng.integers(3))]
+        dtype = ["F32", "F64"][int(rng.integers(2))]
+        out.append((ir, orr, preset, streams, ch, chunk, dtype))
+    return out
+
+
+BATCHES = _batch_cases()
+
+
+@pytest.mark.parametrize("case", BATCHES, ids=[f"{a}-{b}-{p[7:]}-{s}x{c}ch-{k}-{d}" for a, b, p, s, c, k, d in BATCHES])
+def test_batch_sweep_vs_oracle(gar, O, cuda, case):
+    """gar_new_batch: n independent New(config) streams as one lockstep launch; three of the streams
+    (first, middle, last) against the oracle (the others are the same kernels on other columns)."""
+    import torch
+    ir, orr, preset, streams, ch, chunk, dtype = case
+    frames = 6000
+    x = signal(frames, streams * ch, ir, seed=ir + orr + streams)
+    if dtype == "F32":
+        x = x.astype(np.float32).astype(np.float64)
+    dt = torch.float32 if dtype == "F32" else torch.float64
+    r = gar.NewBatch(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=getattr(gar, dtype)), streams)
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(dt).cuda()
+    parts, s = [], 0
+    for n in (chunk_sizes(frames, chunk) if chunk else [frames]):
+        parts.append(r.process_device(xd[s:s + n]).clone())
+        s += n
+    parts.append(r.flush_device(dtype=dt).clone())
+    torch.cuda.synchronize()
+    got = torch.cat(parts).double().cpu().numpy()
+    tol = F64_RMS_TOL if dtype == "F64" else F32_RMS_TOL
+    for st in sorted({0, streams // 2, streams - 1}):
+        want = oracle_new(O, ir, orr, x[:, st * ch:(st + 1) * ch], getattr(O, "P_" + preset[7:].upper()))
+        for c in range(ch):
+            assert got.shape[0] == len(want[c])
+            assert rms(got[:, st * ch + c], want[c]) <= tol
