@@ -32,7 +32,7 @@ fi
 if [ "${CABI:-0}" = 1 ]; then
   timeout -k 10 240 ./tools/cabi_stream 4096 60 2 > $O/cabi_stereo.txt 2>&1 || exit 1
   timeout -k 10 240 ./tools/cabi_stream 4096 10 256 > $O/cabi_256.txt 2>&1 || exit 1
-  tail -3 $O/cabi_stereo.txt $O/cabi_256.txt
+  tail -n 3 $O/cabi_stereo.txt $O/cabi_256.txt
 fi
 if [ "${PROF:-1}" = 1 ]; then
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pmc > $O/prof_bench.log 2>&1 )
