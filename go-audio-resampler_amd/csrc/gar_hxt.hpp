@@ -114,6 +114,10 @@ __device__ __forceinline__ void hxtPut(char* qb, uint32_t dL, int p, int R, int 
 
 __device__ __forceinline__ uint32_t hxtMag(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
+// (r05: the split with v_pk_mul_f32 for the two power-of-two scalings -- 12 instead of 16 VALU per
+// item -- measured slower on every workload, ns256 1.766 vs 1.732 ms, cfg3 0.332 vs 0.317 ms: packed f32
+// next to the compute waves' MFMAs costs more issue than it saves; profiles/r05s_ab_pksplit.txt)
+
 template <int FMT, int NL>
 __device__ __forceinline__ f32x4 hxtItem(const HxtBuf<FMT, NL>& r, int k) {
     if constexpr (FMT == 1) return f32x4{r.a[k].x, r.a[k].y, r.b[k].x, r.b[k].y};
@@ -185,6 +189,11 @@ __device__ GAR_HXT_SLOW_ATTR void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b,
 // interleaves across items, then the ring writes (their per-item / per-lane conditions are branches);
 // split and write per item inside the branches (0) left each item's dependent VALU chain alone in its
 // basic block (r05 stamps: ~730 cycles per item on a loader beside three MFMA waves).
+// GAR_HXT_LOBASE (default): the lo rows' base is its own register per period, so the B-lo reads of
+// every step are base + immediate offset instead of an add of the (runtime) hi/lo distance per step.
+#ifndef GAR_HXT_LOBASE
+#define GAR_HXT_LOBASE 1
+#endif
 #ifndef GAR_HXT_SPLITFIRST
 #define GAR_HXT_SPLITFIRST 1
 #endif
@@ -558,7 +567,11 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
             for (int i = 0; i < n; ++i) {
                 asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
                 const bool last = i + 1 == n;
-                const uint32_t aL = aH + dL, aN = aH + pst, aNL = aN + dL;
+                uint32_t aL = aH + dL;
+#if GAR_HXT_LOBASE
+                asm volatile("" : "+v"(aL));  // lo-row base kept apart: lo reads use aL + offset:imm (no per-step add of dL)
+#endif
+                const uint32_t aN = aH + pst, aNL = aN + dL;
                 f32x4 nA = {0, 0, 0, 0}, nL = nA;
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
