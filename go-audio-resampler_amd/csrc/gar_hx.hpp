@@ -557,7 +557,9 @@ __global__ __launch_bounds__(64 * kHxMaxWaves) void hx_kernel(HxArgs x) {
                 // products); the epilogue of period egi (oA, oL) runs after its first step when epi
                 auto period = [&](f32x4& nA, f32x4& nL, const f32x4& oA, const f32x4& oL, bool epi, int egi, bool first) {
                     asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
-                    const uint32_t aL = aH + dL, aN = aH + gstep, aNL = aN + dL;
+                    uint32_t aL = aH + dL;
+                    asm volatile("" : "+v"(aL));  // lo reads: aL + offset:imm
+                    const uint32_t aN = aH + gstep, aNL = aN + dL;
                     nA = f32x4{0, 0, 0, 0};
                     nL = nA;
 #pragma unroll

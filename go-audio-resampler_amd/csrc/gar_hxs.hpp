@@ -675,7 +675,9 @@ __device__ __forceinline__ void hxsGroups(const HxsArgs& x, const HxsShared& sh_
         // epilogue of period ep (oA, oL) issues after its second step when epi
         auto period = [&](f32x4& nA, f32x4& nL, const f32x4& oA, const f32x4& oL, bool epi, int ep, bool last) {
             asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
-            const uint32_t aL = aH + dL, aN = aH + pstep, aNL = aN + dL;
+            uint32_t aL = aH + dL;
+            asm volatile("" : "+v"(aL));  // lo reads: aL + offset:imm (hxt_kernel r05: -3 .. -6 %)
+            const uint32_t aN = aH + pstep, aNL = aN + dL;
             nA = f32x4{0, 0, 0, 0};
             nL = nA;
 #pragma unroll
@@ -931,9 +933,11 @@ __device__ __forceinline__ void hxsSmallOut(const HxsArgs& x, uint32_t aH, uint3
                                             int rbw, int lane, int sh) {
     const int grp = lane >> 4, l16 = lane & 15;
     f32x4 nA = {0, 0, 0, 0}, nL = nA;
+    uint32_t aL = aH + dL;
+    asm volatile("" : "+v"(aL));  // lo reads: aL + offset:imm
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        const h8v bh = bFragA(aH + 256 * s), bl = bFragA(aH + dL + 256 * s);
+        const h8v bh = bFragA(aH + 256 * s), bl = bFragA(aL + 256 * s);
         nA = mfma16(Ah[s], bh, nA);
         nA = mfma16(Al[s], bh, nA);
         nL = mfma16(Ah[s], bl, nL);
