@@ -2242,6 +2242,35 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
     r->profile = on != 0;
 }
 
+int64_t gar_dev_pool_selftest(int32_t threads, int32_t iters, int32_t channels, int64_t frames) {
+    if (threads < 1 || iters < 0 || channels < 1 || frames < 0) return -1;
+    std::atomic<int64_t> bad{0};
+    auto body = [&](int t) {
+        std::vector<double> src(static_cast<size_t>(channels) * frames), dst(src.size());
+        std::vector<float> mid(src.size());
+        for (size_t i = 0; i < src.size(); ++i) src[i] = static_cast<double>((i * 2654435761u + t) % 65536) / 65536.0 - 0.5;
+        for (int k = 0; k < iters; ++k) {
+            std::fill(dst.begin(), dst.end(), -9.0);
+            gar::forSlices(channels, frames, 12, [&](int c, int64_t lo, int64_t hi) {
+                gar::packChannel<double>(mid.data() + static_cast<size_t>(c) * frames, false,
+                                         src.data() + static_cast<size_t>(c) * frames, lo, hi);
+            });
+            gar::forSlices(channels, frames, 12, [&](int c, int64_t lo, int64_t hi) {
+                gar::unpackChannel<double>(dst.data() + static_cast<size_t>(c) * frames, false,
+                                           mid.data() + static_cast<size_t>(c) * frames, lo, hi);
+            });
+            int64_t b = 0;
+            for (size_t i = 0; i < src.size(); ++i) b += dst[i] != static_cast<double>(static_cast<float>(src[i]));
+            bad += b;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(body, t);
+    body(0);
+    for (auto& x : th) x.join();
+    return bad.load();
+}
+
 void gar_profile_kinds(gar_resampler* r, uint32_t kinds) {
     if (!r) return;
     r->profileKinds = kinds & 0x3fu;

@@ -226,6 +226,12 @@ gar_status gar_profile_launch_stats(gar_resampler *r, int32_t kind, double *min_
  * polyphase_stage.go:300-307 history quirk).  Works on dry-run handles. */
 gar_status gar_stage_state(const gar_resampler *r, int32_t stage, int32_t *fused_plan, int32_t *fused_now);
 
+/* Host self-test of the staging pool the host calls convert through (no GPU): `threads` caller
+ * threads each run `iters` conversion jobs of channels x frames through the pool at once (one job
+ * at a time uses the workers, the others run inline) and check every element.  0 = every element
+ * right; else the number of wrong elements.  For tests (CPU suite; tools/asan_tests.sh with TSan). */
+int64_t gar_dev_pool_selftest(int32_t threads, int32_t iters, int32_t channels, int64_t frames);
+
 /* ---- host-only design introspection (no GPU needed) ----------------------- */
 typedef struct gar_engine_geometry {
     int32_t kind; /* 0 cubic, 1 DFT-only, 2 DFT x2 + polyphase, 3 decimator, 4 pass-through */

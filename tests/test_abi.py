@@ -385,3 +385,16 @@ def test_quick_phase_walk_long_stream(gar, O, i, o):
         r.Process(x)
         total += n
     assert r.FlushSize() == len(e.flush())
+
+
+def test_host_staging_pool_selftest(gar):
+    """The host calls' conversion pool (spinning workers, (generation, index) job tickets, whole-channel
+    jobs): several caller threads at once, every element checked (no GPU needed)."""
+    import ctypes
+    f = gar.lib().gar_dev_pool_selftest
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]
+    assert f(4, 20, 64, 8192) == 0      # many channels: whole channels per job
+    assert f(3, 10, 3, 100000) == 0     # few channels: slices of channels
+    assert f(8, 5, 256, 4096) == 0      # more caller threads than one job: the rest run inline
+    assert f(2, 50, 2, 70000) == 0      # short jobs back to back: workers woken while spinning
