@@ -42,6 +42,9 @@ constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 // SIMD with three MFMA-issuing compute waves; at equal priority the arbiter lets the MFMA stream
 // starve the loaders' VALU (r05 stamps: ~19 cycles per loader VALU instruction), and the loaders
 // are the kernel's critical path.
+#ifndef GAR_HXT_CPRIO  // development: s_setprio of the compute waves (r05u: 1, 2, 3 all within noise of 0)
+#define GAR_HXT_CPRIO 0
+#endif
 #ifndef GAR_HXT_LPRIO
 #define GAR_HXT_LPRIO 0
 #endif
@@ -609,6 +612,7 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
                                            int lane, int nl, int coop, unsigned long long* st) {
     // A of the wave's row block (kept in registers only inside this role: the loaders' registers
     // are the load buffers)
+    if constexpr (GAR_HXT_CPRIO > 0) __builtin_amdgcn_s_setprio(GAR_HXT_CPRIO);
     const HxtRole ro = hxtRole(x, wt);
     const int* pt = x.progs + kBgProgInts * ro.rb;
     const int u0 = uni(pt[4]), rbw = uni(pt[3]);
