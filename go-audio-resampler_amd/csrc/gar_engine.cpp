@@ -996,6 +996,7 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
                     PolyDev p = rt.polyD;
                     p.at0 = before.at;
                     p.u_base = before.u_base;
+                    p.m0 = before.y_count;
                     HIPCHK(timed(x, 4, [&] { return launchPoly(p, usrc, mkOut(out, y0, nout), nout, C, x.s); }));
                 }
                 if (nu > 0) hist_update(x, dv.uh, usrc, c.u_base, c.u_count);
@@ -1081,6 +1082,7 @@ int64_t stageFlush(Ctx& x, int si, const OutView& out) {
                     PolyDev p = rt.polyD;
                     p.at0 = before.at;
                     p.u_base = before.u_base;
+                    p.m0 = before.y_count;
                     HIPCHK(timed(x, 4, [&] { return launchPoly(p, usrc, mkOut(o2, y0, nout), nout, C, x.s); }));
                 }
                 hist_update(x, dv.uh, usrc, c.u_base, c.u_count);

@@ -343,7 +343,9 @@ __device__ __forceinline__ TC pvGet(const typename PolyVec<TC, CG>::V& v, int j)
 // Tap order of output m: k = r, r+1, .., T-1, 0, .., r-1 with r = (m - ph*T) mod 16 (mod T), so
 // the bank rows [ph][k] that 16 consecutive outputs read in one step fall on 16 distinct 16-B LDS
 // bank groups (slot (ph*T + k) mod 16 = (m + i) mod 16) instead of colliding on ph mod 16.  A
-// function of the output alone: every launch geometry sums an output in the same order
+// function of the output's absolute index in the stage's output stream (PolyDev::m0 + the launch-
+// relative index; r05: the launch-relative index made the order, and so the bits, depend on the
+// chunking -- found by the ragged-call sweep): every launch geometry sums an output in the same order
 // (chunk-invariant bits); the reference sums k = 0 .. T-1 (the f32 / f64 tolerances cover it).
 __device__ __forceinline__ int polyRot(int64_t m, int ph, int T) {
     return static_cast<int>((static_cast<unsigned>(m) - static_cast<unsigned>(ph) * static_cast<unsigned>(T)) & 15u) % T;
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc s
         TC acc[CG];
 #pragma unroll
         for (int j = 0; j < CG; ++j) acc[j] = 0;
-        int k = polyRot(m, ph, T);
+        int k = polyRot(p.m0 + m, ph, T);
 #pragma unroll 8
         for (int i = 0; i < T; ++i) {
             const V4 cf = row[k];
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc s
         TC acc[CG];
 #pragma unroll
         for (int j = 0; j < CG; ++j) acc[j] = 0;
-        int k = polyRot(m, ph, T);
+        int k = polyRot(p.m0 + m, ph, T);
         if (wp) {
 #pragma unroll 8
             for (int i = 0; i < T; ++i) {

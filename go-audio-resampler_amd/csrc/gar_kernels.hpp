@@ -112,6 +112,7 @@ struct PolyDev {
     int f64;
     int L, T;
     int64_t step, at0, u_base;  // u_base = global stream index of local history index 0
+    int64_t m0;                 // the stage's absolute output index of the launch's first output (tap rotation)
     const void *a, *b, *c, *d;  // [L][T] reversed, compute dtype
     const void* abcd;           // [L][T][4] the same four banks interleaved (poly_kernel's one-load tap)
 };

@@ -186,6 +186,21 @@ def test_chunking_is_bit_identical(gar, cuda, dtype):  # processinto_test.go:258
                                               chunk_sizes(n, size)), ref)
 
 
+@pytest.mark.parametrize("dtype", ["F32", "F32_EXACT", "F64"])
+@pytest.mark.parametrize("case", [(8000, 11025, 1, "QualityMedium"), (16000, 44100, 2, "QualityHigh"),
+                                  (64000, 176400, 2, "QualityLow"), (37800, 44100, 3, "QualityVeryHigh")])
+def test_chunking_is_bit_identical_fractional_steps(gar, cuda, case, dtype):
+    """Ratios whose polyphase step has fractional bits (poly_kernel, live cubic coefficients): any
+    chunking == one shot, bit for bit (r05: the tap rotation used the launch-relative output index, so
+    chunked and one-shot sums differed in the last bits -- found by the ragged-call sweep)."""
+    ir, orr, ch, q = case
+    dt = getattr(gar, dtype)
+    x = signal(20011, ch, ir, seed=9)
+    one = dev_run(gar, cuda, ir, orr, x, getattr(gar, q), dt)
+    for size in (4096, 1111, 97):
+        np.testing.assert_array_equal(dev_run(gar, cuda, ir, orr, x, getattr(gar, q), dt, chunk_sizes(20011, size)), one)
+
+
 @pytest.mark.parametrize("case", [(48000, 44100, 5, "QualityVeryHigh"), (96000, 44100, 3, "QualityVeryHigh"),
                                   (22050, 44100, 1, "QualityHigh"), (44100, 96000, 4, "QualityLow")])
 def test_chunking_is_bit_identical_f32_pipelines(gar, cuda, case):

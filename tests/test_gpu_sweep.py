@@ -189,6 +189,11 @@ def test_ragged_calls_sweep_vs_oracle(gar, O, cuda, case):
     for c in range(ch):
         assert got.shape[0] == len(want[c]), (c, got.shape, len(want[c]))
         assert rms(got[:, c], want[c]) <= tol
+    # and the same bits as the whole stream in one call (processinto_test.go:258-308)
+    r1 = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=getattr(gar, dtype)))
+    one = torch.cat([r1.process_device(xd), r1.flush_device(dtype=tdt)]).double().cpu().numpy() if frames else got
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got, one)
 
 
 def _pcm_cases(n=40, seed=1616):
@@ -401,3 +406,72 @@ def test_batch_sweep_vs_oracle(gar, O, cuda, case):
         for c in range(ch):
             assert got.shape[0] == len(want[c])
             assert rms(got[:, st * ch + c], want[c]) <= tol
+
+
+def _loud_cases(n=30, seed=6060):
+    rng = np.random.default_rng(int(os.environ.get("GAR_SWEEP_SEED", str(seed))))
+    out = []
+    while len(out) < n:
+        ir, orr = (int(v) for v in rng.choice(RATES, 2))
+        if ir == orr:
+            continue
+        preset = PRESETS[1 + int(rng.integers(len(PRESETS) - 1))]
+        ch = [1, 2, 3, 16][int(rng.integers(4))]
+        nonfinite = bool(rng.random() < 0.4)
+        chunk = [None, 4096, 1111][int(rng.integers(3))]
+        out.append((ir, orr, preset, ch, nonfinite, chunk, int(rng.integers(1 << 30))))
+    return out
+
+
+LOUD = _loud_cases()
+
+
+@pytest.mark.parametrize("case", LOUD, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{'nf' if f else 'loud'}-{k}" for a, b, p, c, f, k, _ in LOUD])
+def test_loud_and_nonfinite_sweep(gar, O, cuda, case):
+    """Samples outside the split-f16 range (|x| >= 16 - 2^-8: runs scaled by 40 .. 1e5, single spikes) and,
+    in some cases, Inf / NaN at random places, on float32 compute: non-finite wherever the oracle is,
+    finite values within the error exact-f32 arithmetic makes on the same signal, and any chunking
+    gives the one-shot bits."""
+    import torch
+    ir, orr, preset, ch, nonfinite, chunk, s0 = case
+    rng = np.random.default_rng(s0)
+    frames = 12000
+    x = signal(frames, ch, ir, seed=s0 % 1000)
+    for _ in range(int(rng.integers(1, 5))):  # loud runs
+        c, t = int(rng.integers(ch)), int(rng.integers(frames - 100))
+        x[t:t + int(rng.integers(1, 100)), c] *= float(rng.choice([40.0, 1000.0, 1e5]))
+    if nonfinite:
+        for v in (np.inf, -np.inf, np.nan)[: int(rng.integers(1, 4))]:
+            x[int(rng.integers(frames)), int(rng.integers(ch))] = v
+    x = x.astype(np.float32).astype(np.float64)
+
+    def run(dtype, ck):
+        r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=dtype))
+        xd = torch.from_numpy(np.ascontiguousarray(x)).float().cuda()
+        parts, s = [], 0
+        for n in (chunk_sizes(frames, ck) if ck else [frames]):
+            parts.append(r.process_device(xd[s:s + n]).clone())
+            s += n
+        parts.append(r.flush_device(dtype=torch.float32).clone())
+        torch.cuda.synchronize()
+        return torch.cat(parts).double().cpu().numpy()
+
+    got = run(gar.F32, chunk)
+    ex = run(gar.F32_EXACT, None)
+    want = oracle_new(O, ir, orr, x, getattr(O, "P_" + preset[7:].upper()))
+    for c in range(ch):
+        w = np.asarray(want[c])
+        assert got.shape[0] == len(w)
+        nf_w, nf_g = ~np.isfinite(w), ~np.isfinite(got[:, c])
+        # every output the reference makes non-finite is non-finite here; on plans that run on plain
+        # MFMA programs (not the split-f16 kernels: e.g. a long f32 decimator) an Inf / NaN sample
+        # under a zero-padded tap of an output's band also gives NaN (0 * Inf): at most the padding
+        # (< 2 steps of 32 rows) per non-finite input sample of the channel -- DESIGN.md section 5
+        assert not (nf_w & ~nf_g).any(), c
+        n_in = int((~np.isfinite(x[:, c])).sum())
+        assert int((nf_g & ~nf_w).sum()) <= 64 * n_in, (c, int((nf_g & ~nf_w).sum()))
+        fin = ~nf_w & ~nf_g
+        fe = np.isfinite(ex[:, c]) & fin
+        assert rms(got[fin, c], w[fin]) <= max(3.0 * rms(ex[fe, c], w[fe]), F32_RMS_TOL), c
+    if chunk:
+        np.testing.assert_array_equal(got, run(gar.F32, None))

@@ -33,6 +33,12 @@ for dt in os.environ.get("SD_DT", "F32,F64").split(","):
         bad = np.nonzero(np.abs(got[:, 0] - want[0]) > 1e-4)[0] if got.shape[0] == len(want[0]) else []
         res[f"{dt}-{'chunk' if ck else 'one'}"] = {"rms": max(e), "n": got.shape[0], "first_bad": int(bad[0]) if len(bad) else None,
                                                    "nbad": int(len(bad)), "sizes": sizes[:6]}
+        if ck is None:
+            ref_one = got
+        elif got.shape == ref_one.shape:
+            diff = np.nonzero((got != ref_one).any(axis=1))[0]
+            res[f"{dt}-chunk"]["bits_differ_rows"] = int(len(diff))
+            res[f"{dt}-chunk"]["first_diff_row"] = int(diff[0]) if len(diff) else None
 print(json.dumps(res))
 ''' % (ROOT, os.path.join(ROOT, "go-audio-resampler_amd"), os.path.join(ROOT, "tests"))
 
