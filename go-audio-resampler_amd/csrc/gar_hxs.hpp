@@ -632,7 +632,9 @@ __device__ __forceinline__ void hxsGroups(const HxsArgs& x, const HxsShared& sh_
         const f32x4 y = hxScale(oA, oL, sh);
         if (dbg & 2) return;
         if constexpr (FAST) {
-            hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride, y, lane);
+            // periods past the chunk (ngroups * G > Np) belong to the next chunk's column, whose
+            // fixup owns their loud outputs: storing them here raced with it (r05 loud sweep, C=3)
+            if (p < x.Np) hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride, y, lane);
         } else {
             const int64_t a = aCol + p;
             const int64_t o0 = a * x.Pc + oRow0;

@@ -120,6 +120,30 @@ def test_short_call_after_long_history_f32_decimator(gar, O, cuda):
         assert rms(got[:, c], want[c]) <= F32_RMS_TOL
 
 
+@pytest.mark.parametrize("ch", [3, 5])
+def test_loud_samples_odd_channels_chunk_overlap(gar, O, cuda, ch):
+    """Regression (found by the loud sweep): 8k -> 88.2k QualityHigh, 3 or 5 channels, loud samples in
+    channel 0.  The third x2 stage runs hxs_kernel with Np = 9 periods per chunk in groups of G = 6, so
+    a column's second group computes 3 periods of the next chunk; its fast epilogue stored them too,
+    without the loud fixup the next chunk's own column applies -- a race between the two workgroups
+    (wrong outputs, different on every run).  Two runs: equal bits, both within the f32 bound."""
+    x = signal(12000, ch, 8000, seed=5)
+    x[3000:3040, 0] *= 1e5
+    x[7000, 0] = 40.0
+    x = x.astype(np.float32).astype(np.float64)
+    want = oracle_new(O, 8000, 88200, x, O.P_HIGH)
+    runs = []
+    for _ in range(2):
+        r = gar.New(gar.Config(8000, 88200, ch, gar.QualityHigh, ComputeDtype=gar.F32))
+        outs = r.ProcessMulti([x[:, c] for c in range(ch)])
+        tails = r.FlushMulti()
+        runs.append([np.concatenate([outs[c], tails[c]]) for c in range(ch)])
+    for c in range(ch):
+        assert np.array_equal(runs[0][c], runs[1][c])
+        w = np.asarray(want[c])
+        assert np.abs(runs[0][c] - w).max() <= 1e-3 * max(1.0, np.abs(w).max())
+
+
 def _odd_cases(n=60, seed=31337):
     """Arbitrary integer rates (not from the usual families): ratios with fractional polyphase
     steps (poly_kernel, live cubic coefficients), long rational periods and the Quick cubic stage."""
