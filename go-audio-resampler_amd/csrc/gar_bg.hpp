@@ -738,7 +738,9 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
         for (int s = 0; s < NS; ++s) {
             B[s] = win[nb + q * (Qc + pad) + rem];
             rem += 4;
-            if (rem >= Qc) { rem -= Qc; ++q; }
+            // a step of 4 rows spans several macro periods when Qc < 4 (integer upsamplers, Qc = 1:
+            // r05 sweep, 11025 -> 176400 engine seam in 4096-frame calls)
+            while (rem >= Qc) { rem -= Qc; ++q; }
         }
         V acc0 = {0, 0, 0, 0}, acc1 = acc0;
 #pragma unroll

@@ -120,6 +120,27 @@ def test_short_call_after_long_history_f32_decimator(gar, O, cuda):
         assert rms(got[:, c], want[c]) <= F32_RMS_TOL
 
 
+@pytest.mark.parametrize("ir,orr,q", [(11025, 176400, 2), (8000, 128000, 3), (22050, 176400, 2), (11025, 88200, 4)])
+def test_f64_integer_upsampler_short_calls(gar, O, cuda, ir, orr, q):
+    """Regression (sweep seed 21): an engine-seam integer upsampler (x16 / x8 DftOnly, Qc = 1) on float64
+    in short calls and its Flush run the small-launch time-major kernel (bg_rt_kernel), whose B-row walk
+    advanced 4 rows per step with one wrap -- right for Qc >= 3, garbage (1e200+) for Qc = 1 or 2."""
+    frames = 9000
+    x = signal(frames, 1, ir, seed=ir + 3 * orr + q)[:, 0]
+    r = gar.EngineNewResampler(ir, orr, q, gar.F64)
+    e = O.Engine(ir, orr, q)
+    got, want, s = [], [], 0
+    for n in chunk_sizes(frames, 4096):
+        got.append(r.Process(x[s:s + n]))
+        want.append(e.process(x[s:s + n]))
+        s += n
+    got.append(r.Flush())
+    want.append(e.flush())
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert got.shape == want.shape
+    assert rms(got, want) <= F64_RMS_TOL
+
+
 @pytest.mark.parametrize("ch", [3, 5])
 def test_loud_samples_odd_channels_chunk_overlap(gar, O, cuda, ch):
     """Regression (found by the loud sweep): 8k -> 88.2k QualityHigh, 3 or 5 channels, loud samples in
@@ -498,4 +519,16 @@ def test_loud_and_nonfinite_sweep(gar, O, cuda, case):
         fe = np.isfinite(ex[:, c]) & fin
         assert rms(got[fin, c], w[fin]) <= max(3.0 * rms(ex[fe, c], w[fe]), F32_RMS_TOL), c
     if chunk:
-        np.testing.assert_array_equal(got, run(gar.F32, None))
+        one = run(gar.F32, None)
+        if not nonfinite:
+            np.testing.assert_array_equal(got, one)
+        else:
+            # the padded-tap NaNs sit where the MFMA tiles fall, which a call boundary moves (seed 11:
+            # 192k -> 88.2k VeryHigh, 4096-frame calls): same bits wherever both are finite, and the
+            # one-shot run meets the same non-finite contract
+            both = np.isfinite(got) & np.isfinite(one)
+            np.testing.assert_array_equal(got[both], one[both])
+            for c in range(ch):
+                nf_w, nf_o = ~np.isfinite(np.asarray(want[c])), ~np.isfinite(one[:, c])
+                assert not (nf_w & ~nf_o).any(), c
+                assert int((nf_o & ~nf_w).sum()) <= 64 * int((~np.isfinite(x[:, c])).sum()), c
