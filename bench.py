@@ -47,7 +47,7 @@ PEAK_F16_MATRIX_TFLOPS = 2500.0  # dense
 PEAK_F64_MATRIX_TFLOPS = 78.6
 # reference-algorithm flops per input sample
 REF_ALGO_FLOPS = {"cfg2": 1017.6, "ns256": 1017.6, "cfg4": 1017.6, "cfg3": 1169.0, "cfg5": 1807.6, "poly": None,
-                  "quick": None, "pcm16": 1017.6}
+                  "quick": None, "pcm16": 1017.6, "cfg2_f64": 1017.6, "ns256_f64": 1017.6}
 # New path: preset -> precision -> engine quality (stages.go:54-70, pipeline_builder.go:76-100)
 ENGINE_Q = {"High": lambda g: g.Engine24Bit, "VeryHigh": lambda g: g.Engine32Bit, "Quick": lambda g: g.EngineQuick}
 
@@ -70,6 +70,17 @@ WORKLOADS = {
                  seconds=60.0, io="f64", compute="F64", streams=1, scaling="weak", chunk=4800,
                  desc="BASELINE configs[4]: 8-channel float64 96k->44.1k QualityVeryHigh multi-stage pipeline "
                       "(decimator x1/2 -> DFT x2 -> polyphase), 60 s streamed in 4800-frame ProcessInto chunks"),
+    # the same two geometries at the reference New path's own arithmetic: float64 compute of the
+    # float32 streams (constant.go:161-199 converts to float64, runs the float64 engine), f64 I/O so the
+    # 1e-12 RMS bar is measurable; f64 MFMA-bound (bg_kernel, v_mfma_f64_16x16x4_f64)
+    "cfg2_f64": dict(name="cfg2_f64_stereo_f64_44k1_48k_q24_600s", ir=44100, orr=48000, ch=2, preset="High",
+                     seconds=600.0, io="f64", compute="F64", streams=1, scaling="weak", chunk=0,
+                     desc="cfg2 geometry computed in float64 (the reference's own arithmetic), f64 I/O, 600 s "
+                          "stereo stream per GPU, one Process+Flush"),
+    "ns256_f64": dict(name="ns256_f64_256ch_f64_44k1_48k_q24_60s", ir=44100, orr=48000, ch=256, preset="High",
+                      seconds=60.0, io="f64", compute="F64", streams=1, scaling="weak", chunk=0,
+                      desc="north_star geometry computed in float64 (the reference's own arithmetic), f64 I/O, "
+                           "256 ch x 60 s per GPU, one Process+Flush"),
     # x != 0 polyphase (live cubic coefficients, poly_kernel) and QualityQuick (cubic_kernel)
     "poly": dict(name="poly_stereo_f32_16k_44k1_q24_600s", ir=16000, orr=44100, ch=2, preset="High", seconds=600.0,
                  io="f32", compute="F32", streams=1, scaling="weak", chunk=0, kind_bytes={4: 4 * (4 + 2.75625)},
@@ -208,7 +219,8 @@ def front_keys(line):
     keys, then the dominant kernel's per-launch time and roofline fraction, the streaming-call
     figures and the CPU baseline, flat; everything else after them."""
     roof = line.get("roofline") or {}
-    st = line.get("streaming") or {}
+    st = (line.get("secondary") or {}).get("stream4096") or {}
+    stb = (line.get("secondary") or {}).get("stream4096_batch1024") or {}
     s256 = line.get("streaming_256ch") or {}
     cpu = line.get("cpu_baseline") or {}
     flat = {
@@ -218,6 +230,8 @@ def front_keys(line):
         "stream_dev_us_per_call": (st.get("device_api") or {}).get("us_per_call"),
         "stream_host_us_per_call": (st.get("host_cabi") or {}).get("us_per_call"),
         "stream_256ch_host_ms_per_call": s256.get("ms_per_call"),
+        "stream_batch1024_dev_us_per_call": (round(stb["ms_per_step"] * 1e3, 2) if stb.get("ms_per_step") else None),
+        "stream_batch1024_msamples_per_s": stb.get("value"),
         "cpu_baseline_msamples_per_s": cpu.get("value"),
         "cpu_baseline_cores": cpu.get("cores"),
     }
@@ -352,7 +366,8 @@ def pmc_traffic(args, workload, kernel_keys):
 # global load per lane and step for A and B (gar_bg.hpp bg_rb_kernel), each lane of a B load on its
 # own 64-B row of the interleaved 8-channel stream -- the x2 streaming calibration is an upper bound
 # there, so bench also reports the uncorrected read bytes)
-LOAD_WIDTH = {"cfg2": 8, "cfg4": 8, "ns256": 16, "cfg3": 16, "pcm16": 4, "cfg5": 8, "poly": 4, "quick": 4}
+LOAD_WIDTH = {"cfg2": 8, "cfg4": 8, "ns256": 16, "cfg3": 16, "pcm16": 4, "cfg5": 8, "poly": 4, "quick": 4,
+              "cfg2_f64": 4, "ns256_f64": 4}  # bg_kernel: LDS-DMA global_load_lds_dword, 4 B per lane
 KIND_NAMES = {0: "fused DFTx2->polyphase FIR", 1: "DFT FIR", 2: "decimator FIR", 3: "fused FIR (flush)",
               4: "polyphase with live cubic coefficients (poly_kernel)", 5: "QualityQuick cubic stage (cubic_kernel)"}
 # profile kind -> engine kind of the stage it runs (gar_engine_geometry.kind: 1 DFT-only, 2 DFT+poly, 3 decim, 0 cubic)
@@ -366,11 +381,11 @@ FETCH_CORRECTION = {16: 2.0, 8: 2.0, 4: 2.0}
 
 def secondary_default(primary, world):
     """Workloads timed beside the primary line (each with its own ms, roofline and PMC traffic):
-    the north-star 256-ch stream, BASELINE configs[2], configs[4] and -- the scaling config,
-    at every world size -- configs[3]."""
+    the north-star 256-ch stream, BASELINE configs[2], configs[4], the cfg2 / north-star geometries
+    at the reference's float64 arithmetic and -- the scaling config, at every world size -- configs[3]."""
     if primary != "cfg2":
         return []
-    return ["ns256", "cfg3", "cfg5", "cfg4"] if world == 1 else ["cfg4"]
+    return ["ns256", "cfg3", "cfg5", "cfg4", "cfg2_f64", "ns256_f64"] if world == 1 else ["cfg4"]
 
 
 def run_workload(key, args, steps, warmup, world, rank, dev, primary):
@@ -492,6 +507,7 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
         r.profile(False)
 
     local_samples = frames * C * steps
+    local_ms = (t1 - t0) / steps * 1e3
     elapsed, total_samples = reduce_stats(t1 - t0, local_samples, dev if not dry else None)
     _, total_out = reduce_stats(0.0, (n_proc + n_tail) * C, dev if not dry else None)
 
@@ -528,6 +544,7 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
         },
         "output_samples_total": int(total_out),
         "input_samples_total": int(total_samples / steps),
+        "local_ms_per_step": round(local_ms, 4),
     }
     kernel_keys = []
     if not dry:
@@ -542,8 +559,8 @@ def run_workload(key, args, steps, warmup, world, rank, dev, primary):
                         "products as three f16 MFMA terms of 22-bit split operands, f32 accumulation "
                         "(error at the level of exact-f32 arithmetic)" if w["compute"] == "F32"
                         else "f64 I/O and f64 MFMA (v_mfma_f64_16x16x4_f64)")
-        if primary and rank == 0 and not args.no_streaming and w["compute"] == "F32" and w["scaling"] == "weak" \
-                and w["io"] == "f32":
+        if primary and rank == 0 and world == 1 and not args.no_streaming and w["compute"] == "F32" \
+                and w["scaling"] == "weak" and w["io"] == "f32":
             obj["streaming"] = time_streaming(gar, torch, w, x, C, dev)
         del x, y, yf
     del r
@@ -641,31 +658,26 @@ def roofline(w, key, gar, r, prof, steps, frames, C, n_proc, n_tail):
     else:
         # f64: MFMA-bound (f64 matrix rate); useful flops of the dominant stage's own design
         flops_step = 2.0 * st_geom.useful_macs_per_output * st_out
-        if dom == 0 and not prof[2][1] and sidx > 0 and geoms[sidx - 1][1].kind == 3:
-            # pair launches (bg_pair_kernel): the decimator stage before the composite runs inside the
-            # same launch, so its useful flops belong to it too
-            flops_step += 2.0 * geoms[sidx - 1][1].useful_macs_per_output * st_in
         fl_launch = flops_step / per_step
         achieved = fl_launch / launch_s / 1e12 if launches else None
         roof = {"bound": "mfma", "achieved": round(achieved, 2) if achieved else None,
                 "peak": PEAK_F64_MATRIX_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F64_MATRIX_TFLOPS, 4) if achieved else None}
-        paired = dom == 0 and not prof[2][1] and sidx > 0 and geoms[sidx - 1][1].kind == 3
         chunked = bool(w["chunk"])
         # the kernel that runs the dominant kind: small launches of a chunked stream run the decimator
         # (<= 2 row blocks) on bg_rt_kernel and the composite on bg_rb_kernel (gar_kernels.hip
         # bgSmallGrid); one-shot streams run bg_kernel
-        small = ("bg_rt_kernel" if dom == 2 else "bg_pair_kernel" if paired else "bg_rb_kernel")
+        small = "bg_rt_kernel" if dom == 2 else "bg_rb_kernel"
         kernel_keys = (["poly_kernel"] if dom == 4 else [small] if chunked else ["bg_kernel"])
-        kern = ('poly_kernel<double>' if dom == 4 else
-                ('bg_pair_kernel<double> (decimator items + bg_rb_kernel<double>' if paired else
-                 f'{small}<double>' if chunked else 'bg_kernel<double>'))
-        kname = (f"{kern} ({KIND_NAMES[dom]}, stage {sidx}: {48000:g}->{48000 * st_ratio:g} Hz engine"
-                 f"{', with the decimator stage before it in the same launch)' if paired else ''}, v_mfma_f64_16x16x4_f64)")
-        # a pair launch reads the decimator's input (the stream) and writes the composite's output
-        algo_unit_bytes = ((frames * C if paired else st_in) + st_out) * 8 / per_step
+        kern = ('poly_kernel<double>' if dom == 4 else f'{small}<double>' if chunked else 'bg_kernel<double>')
+        kname = (f"{kern} ({KIND_NAMES[dom]}, stage {sidx}: {48000:g}->{48000 * st_ratio:g} Hz engine, "
+                 "v_mfma_f64_16x16x4_f64)")
+        algo_unit_bytes = (st_in * in_bytes + st_out * in_bytes) / per_step
         roof["useful_macs_per_output"] = round(st_geom.useful_macs_per_output, 2)
         roof["stage_outputs_per_step"] = int(st_out)
+        if launches:  # the same launch against HBM (its stage's input read once + output written once)
+            roof["hbm_gbps"] = round(algo_unit_bytes / launch_s / 1e9, 1)
+            roof["hbm_frac"] = round(algo_unit_bytes / launch_s / 1e9 / PEAK_HBM_GBPS, 4)
     roof["ref_algo_flops_per_input_sample"] = REF_ALGO_FLOPS[key]
     roof["kernel_ms_by_kind"] = {KIND_NAMES[k]: round(prof[k][0] / steps, 4) for k in prof if prof[k][1]}
     roof["launches_per_step_by_kind"] = {KIND_NAMES[k]: prof[k][1] / steps for k in prof if prof[k][1]}
@@ -757,6 +769,8 @@ def main():
     ap.add_argument("--secondary", default="auto",
                     help="comma list of workloads timed beside the primary line, 'auto' or 'none'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
+                    help="CPU work of the baseline's single-thread sample (bounded; the all-core run is shorter)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live PMC traffic passes")
     ap.add_argument("--no-streaming", action="store_true", help="skip the chunked drop-in timing")
     ap.add_argument("--check-seconds", type=float, default=5.0, help="prefix (and suffix) checked against the oracle")
@@ -785,23 +799,32 @@ def main():
     ranks = rank_devices(world, rank, dev, args.dry_run)
     line, keys = run_workload(args.workload, args, args.steps, args.warmup, world, rank, dev, primary=True)
     line["ranks"] = ranks
-    if rank == 0 and world == 1 and not args.no_pmc and not args.dry_run:
-        attach_traffic(line, args, args.workload, keys)
-    line["cpu_baseline"] = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
-        line["cpu_baseline"] = cpu_baseline(WORKLOADS[args.workload])
-    if rank == 0 and world == 1 and not args.no_streaming and not args.dry_run and args.workload == "cfg2":
-        line["streaming_256ch"] = time_streaming_host(WORKLOADS["ns256"], dev)
+    line["per_rank"] = per_rank(line, world)
     sec = (secondary_default(args.workload, world) if args.secondary == "auto"
            else [] if args.secondary == "none" else [k for k in args.secondary.split(",") if k])
     if sec:
         line["secondary"] = {}
         for key in sec:
-            obj, keys = run_workload(key, args, min(args.steps, 10), min(args.warmup, 2), world, rank, dev,
-                                     primary=False)
+            obj, skeys = run_workload(key, args, min(args.steps, 10), min(args.warmup, 2), world, rank, dev,
+                                      primary=False)
+            obj["per_rank"] = per_rank(obj, world)
             if rank == 0 and world == 1 and not args.no_pmc and not args.dry_run:
-                attach_traffic(obj, args, key, keys)
+                attach_traffic(obj, args, key, skeys)
             line["secondary"][key] = obj
+    # after every timed region and collective: rank 0's own measurements (the other ranks are done)
+    # world > 1: a child run on rank 0's GPU of the same per-rank work (weak-scaled workloads only)
+    if rank == 0 and not args.no_pmc and not args.dry_run and (world == 1 or WORKLOADS[args.workload]["scaling"] == "weak"):
+        attach_traffic(line, args, args.workload, keys)
+    if rank == 0 and not args.no_streaming and not args.dry_run and args.workload == "cfg2":
+        line.setdefault("secondary", {})
+        st = line.pop("streaming", None)
+        if st:
+            line["secondary"]["stream4096"] = streaming_object(st, WORKLOADS["cfg2"])
+        line["streaming_256ch"] = time_streaming_host(WORKLOADS["ns256"], dev)
+        line["secondary"]["stream4096_batch1024"] = time_streaming_batch(dev)
+    line["cpu_baseline"] = None
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(WORKLOADS[args.workload], target_s=args.cpu_baseline_seconds)
     if args.dry_run:
         line["dry_run"] = True
     if rank == 0:
@@ -810,6 +833,31 @@ def main():
         import torch.distributed as dist
         dist.destroy_process_group()
 
+
+def per_rank(obj, world):
+    """Every rank's own step time and dominant-kernel events (all_gather_object when world > 1)."""
+    roof = obj.get("roofline") or {}
+    me = {"rank": int(os.environ.get("RANK", "0")), "local_ms_per_step": obj.get("local_ms_per_step"),
+          "kernel_ms_per_launch": roof.get("kernel_ms_per_launch"),
+          "kernel_ms_min_median_max": roof.get("kernel_ms_min_median_max"), "launches": roof.get("launches"),
+          "frac": roof.get("frac")}
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, me)
+    return out
+
+
+def streaming_object(st, w):
+    """The 4096-frame drop-in pattern as a workload object of its own (metric / value / ms_per_step =
+    one call), device API figures first, the host C-ABI (PCIe-inclusive) beside them."""
+    dv = st["device_api"]
+    return {"metric": f"Msamples/s resampled (float32, {w['ir'] / 1000:g}k→{w['orr'] / 1000:g}k Quality{w['preset']}, "
+                      f"{w['ch']} ch, 4096-frame ProcessInto calls, device API)",
+            "value": dv["value"], "unit": "Msamples/s", "ms_per_step": round(dv["us_per_call"] / 1e3, 5),
+            "step": "one 4096-frame gar_process_device call", "higher_is_better": True, "dtype": "f32",
+            "data": "synthetic", "device_api": dv, "host_cabi": st["host_cabi"], "chunk_frames": st["chunk_frames"]}
 
 def time_streaming(gar, torch, w, x, C, dev, seconds=60.0):
     """The reference's own usage pattern (processinto_bench_test.go:12-205): a stream fed in
@@ -898,6 +946,57 @@ def time_streaming(gar, torch, w, x, C, dev, seconds=60.0):
                       "sample": f"{hs:.0f} s, gar_process_multi_f64 per chunk from planar float64 host buffers "
                                 "(H2D + launches + D2H + synchronise per call, PCIe-inclusive)"},
     }
+
+
+def time_streaming_batch(dev, streams=1024, seconds=10.0, chunk=4096):
+    """The reference's call size on the shape where the GPU pays: `streams` independent stereo
+    44.1k->48k QualityHigh streams (one NewBatch, BASELINE configs[3]'s streams) fed together in
+    4096-frame ProcessInto calls through the device API (one launch per call for all streams), inputs
+    in HBM, one synchronise at the end (processinto_bench_test.go:12-205's chunk size,
+    constant.go:223-249's independent channels)."""
+    import ctypes as Ct
+    import gar
+    import torch
+    w = WORKLOADS["cfg4"]
+    C = 2 * streams
+    frames = int(seconds * w["ir"])
+    x = synth_device(torch, frames, C, 777, w["ir"], torch.float32)
+    r = gar.NewBatch(gar.Config(w["ir"], w["orr"], 2, gar.QualityHigh, ComputeDtype=gar.F32, Device=dev.index), streams)
+    y = torch.empty((int(frames * w["orr"] / w["ir"]) + 64 * (frames // chunk + 2), C), dtype=torch.float32, device=dev)
+    L = gar.lib()
+    st = Ct.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    es = y.element_size() * C
+    calls = [(Ct.c_void_p(x[s:].data_ptr()), min(chunk, frames - s)) for s in range(0, frames, chunk)]
+    got = Ct.c_int64(0)
+    pgot = Ct.byref(got)
+
+    def dev_pass():
+        r.Reset()
+        o = 0
+        for p, n in calls:
+            rc = L.gar_process_device(r._h, p, gar.F32, x.stride(0), x.stride(1), n, C, Ct.c_void_p(y.data_ptr() + o * es),
+                                      gar.F32, y.stride(0), y.stride(1), y.shape[0] - o, pgot, st)
+            if rc != 0:
+                raise RuntimeError(f"gar_process_device: {rc}")
+            o += got.value
+        r.flush_device()
+        return o
+
+    dev_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev_pass()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out = {"metric": f"Msamples/s resampled (float32, 44.1k→48k QualityHigh, {streams} stereo streams, 4096-frame "
+                     "ProcessInto calls, device API)",
+           "value": round(frames * C / dt / 1e6, 2), "unit": "Msamples/s", "ms_per_step": round(dt / len(calls) * 1e3, 5),
+           "step": f"one 4096-frame gar_process_device call of a {streams}-stream NewBatch ({C} channels)",
+           "higher_is_better": True, "dtype": "f32", "data": "synthetic", "calls": len(calls), "streams": streams,
+           "sample": f"{seconds:g} s per stream, {len(calls)} calls + flush, inputs in HBM, one synchronise at the end"}
+    del x, y, r
+    torch.cuda.empty_cache()
+    return out
 
 
 def time_streaming_host(w, dev, calls=40, chunk=4096):

@@ -56,6 +56,66 @@ __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, T
     else static_cast<float*>(o.out)[e] = static_cast<float>(v);
 }
 
+// ---- non-finite samples on the plain MFMA programs ---------------------------------------------
+// The reference multiplies only the real taps of an output's window (dft_stage.go:259 / :531,
+// polyphase_stage.go:288), so an Inf / NaN sample makes exactly the outputs whose real window holds
+// it non-finite.  The MFMA programs also multiply the zero-padded taps of a row block's band, and
+// 0 * Inf = NaN.  So every kernel here stages a non-finite sample as 0 -- each output then carries the
+// value its band gives with that sample zero, whatever the call boundaries, so chunked == one-shot
+// bit for bit -- and records where it was; after the item's stores, the outputs whose REAL window
+// holds a non-finite sample are recomputed over their real taps in f64 in the reference's order
+// (bgNfFixOne: two stages for DFT x2 (*) polyphase composites, as hxsExact does for the split-f16
+// kernels), which gives the reference's NaN / +-Inf for each of them and touches nothing else.
+__device__ __forceinline__ bool bgFinite(double v) { return __builtin_isfinite(v); }
+__device__ __forceinline__ bool bgFinite(float v) { return __builtin_isfinite(v); }
+
+// Output (a, r) of channel c: recomputed and stored when its real window holds a non-finite sample.
+template <class TC>
+__device__ __noinline__ void bgNfFixOne(const BgDev& p, const SrcDesc& src, const OutDesc& od, int64_t a, int r, int c) {
+    const int64_t o = a * p.Pc + r;
+    if (o < od.o_lo || o >= od.o_hi) return;
+    const int* xi = p.xInfo;
+    const int64_t t = a * p.Qc + xi[r];
+    const int len = xi[p.Pc + r];
+    const double* row = p.xRows + static_cast<size_t>(r) * p.xRowMax;
+    double s = 0.0, z = 0.0;
+    for (int k = 0; k < len; ++k) {
+        const double v = static_cast<double>(srcRead<TC>(src, t + k, c));
+        s += row[k] * v;
+        z += v * 0.0;
+    }
+    if (z == z) return;  // the real window is finite: the MFMA value stands
+    if (p.xTwoStage) {   // u = DFT x2 of the window, then the polyphase row (dft_stage.go:259, polyphase_stage.go:288)
+        const int ph = xi[2 * p.Pc + r], par = xi[3 * p.Pc + r], T1 = p.xT1, T2 = p.xT2;
+        const double* pa = p.xPolyA + static_cast<size_t>(ph) * T2;
+        double y = 0.0;
+        for (int k2 = 0; k2 < T2; ++k2) {
+            const int q = par + k2;
+            const double* cq = p.xDftC + static_cast<size_t>(q & 1) * T1;
+            double u = 0.0;
+            for (int k1 = 0; k1 < T1; ++k1) u += cq[k1] * static_cast<double>(srcRead<TC>(src, t + (q >> 1) + k1, c));
+            y += pa[k2] * u;
+        }
+        s = y;
+    }
+    outWrite<TC>(od, o, c, static_cast<TC>(s));
+}
+
+// The outputs (a0 + i, r), i < na, r0 <= r < r1, of channel c whose real window (rows i*Qc + off[r]
+// .. + len[r] relative to input a0*Qc) meets the rows [lo, hi] where non-finite samples were staged;
+// thread tid of nth.
+template <class TC>
+__device__ void bgNfFixRange(const BgDev& p, const SrcDesc& src, const OutDesc& od, int64_t a0, int na, int r0, int r1,
+                             int c, int lo, int hi, int tid, int nth) {
+    const int nr = r1 - r0;
+    for (int idx = tid; idx < na * nr; idx += nth) {
+        const int i = idx / nr, r = r0 + (idx - i * nr);
+        const int w0 = i * p.Qc + p.xInfo[r], w1 = w0 + p.xInfo[p.Pc + r];
+        if (w1 <= lo || w0 > hi) continue;
+        bgNfFixOne<TC>(p, src, od, a0 + i, r, c);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Banded GEMM.  Geometry (host computed in launchBg):
 //   macro period a covers outputs [a*Pc, (a+1)*Pc) and reads inputs starting
@@ -73,6 +133,7 @@ __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, T
 #define GAR_BG_DEV 0
 #endif
 constexpr bool kBgDev = GAR_BG_DEV;
+constexpr size_t kBgStaticLds = 1152;  // bg_kernel's static LDS (nfFlag / nfLo / nfHi: 1032 B), rounded up
 constexpr int kBgProfWords = 64;
 
 struct BgGrid {
@@ -367,11 +428,44 @@ __device__ __forceinline__ void segStore(const ProgU& pu, int j, const typename 
 }
 
 // B fragment of program step s: LDS tile, or global memory (GLOBAL_B).
+// (global-B: a non-finite sample is read as 0 and flagged in nf; LDS tiles were cleaned by bgNfScan)
 template <class TC, bool GB>
 __device__ __forceinline__ TC fetchB(const TC* bp, const ProgU& pu, int s, const SrcDesc& src, int64_t tb, int c,
-                                     bool colOk, bool same, const void* dummy) {
-    if constexpr (GB) return colOk ? srcRead<TC>(src, tb + selK(pu, s) + 4 * s, c) : TC(0);
-    else return bp[selU(pu, s) + 64 * s];
+                                     bool colOk, bool same, const void* dummy, bool& nf) {
+    if constexpr (GB) {
+        const TC v = colOk ? srcRead<TC>(src, tb + selK(pu, s) + 4 * s, c) : TC(0);
+        const bool ok = bgFinite(v);
+        nf |= !ok;
+        return ok ? v : TC(0);
+    } else {
+        return bp[selU(pu, s) + 64 * s];
+    }
+}
+
+// Non-finite samples of one LDS sub-tile: the pieces this wave staged (j = wt mod nwt; lane l of a
+// piece wrote dword l) are checked once they have landed; a non-finite element is set to 0 and its
+// (column, row) recorded in this block's parity slot (nfLo / nfHi per column, nfFlag).
+template <class TC>
+__device__ __forceinline__ void bgNfScan(TC* sub, const BgGrid& g, int cg, int wt, int lane, int par, int* nfFlag,
+                                         int (*nfLo)[64], int (*nfHi)[64]) {
+    constexpr int rowsPerPiece = sizeof(TC) == 8 ? 2 : 4;
+    const int np = tilePieces<TC>(g);
+    const int e = sizeof(TC) == 8 ? (lane >> 1) : lane;  // element (row e >> 4, column e & 15) of the piece
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces landed (LDS-DMA: vmcnt; gathered stores: lgkmcnt)
+    bool any = false;
+#pragma unroll 4
+    for (int j = wt; j < np; j += g.nwt) {
+        TC* q = sub + static_cast<size_t>(j) * rowsPerPiece * 16 + e;
+        const TC v = *q;
+        if (__builtin_expect(!bgFinite(v), 0)) {
+            *q = TC(0);
+            const int col = cg * 16 + (e & 15), row = j * rowsPerPiece + (e >> 4);
+            atomicMin(&nfLo[par][col], row);
+            atomicMax(&nfHi[par][col], row);
+            any = true;
+        }
+    }
+    if (any) nfFlag[par] = 1;
 }
 
 // In-loop segment boundary: bank the running sum (stores happen after the loop).
@@ -405,6 +499,13 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     const TC* Aimg = static_cast<const TC*>(p.A);
     const bool same = srcSameType<TC>(src);
 
+    // non-finite samples staged per block parity (bgNfScan): flag + row range per column
+    __shared__ int nfFlag[2], nfLo[2][64], nfHi[2][64];
+    for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) { (&nfLo[0][0])[i] = 0x7fffffff; (&nfHi[0][0])[i] = -1; }
+    if (threadIdx.x < 2) nfFlag[threadIdx.x] = 0;
+    __syncthreads();
+    bool nfl = false;  // global-B: this lane read a non-finite sample in the current block
+
     TC A[NS];
     if (SINGLE && wt < g.nprog) {
 #pragma unroll
@@ -416,7 +517,10 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     int q = 0;  // macro-period iteration counter (partial-slot parity)
     for (int it = 0; b < g.nblocks; b += gridDim.x, ++it) {
         TC* tile = tiles + static_cast<size_t>(it & 1) * tileElems + cg * subElems;
+        if (!GLOBAL_B) bgNfScan<TC>(tile, g, cg, wt, lane, it & 1, nfFlag, nfLo, nfHi);
         __syncthreads();  // this tile's DMA landed (vmcnt) + the other buffer is free
+        // read right after the barrier: the slot of this parity is written again only after the next one
+        const bool nfB = !GLOBAL_B && nfFlag[it & 1] != 0;
         const int bn = b + gridDim.x;
         const bool pre = !GLOBAL_B && bn < g.nblocks && !(g.dbg & 1);
         TC* ntile = tiles + static_cast<size_t>((it + 1) & 1) * tileElems + cg * subElems;
@@ -456,12 +560,12 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                     TC bA[PF], bB[PF];
 #pragma unroll
                     for (int j = 0; j < PF; ++j)
-                        if (j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + j, src, tb, c, colOk, same, Aimg);
+                        if (j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + j, src, tb, c, colOk, same, Aimg, nfl);
 #pragma unroll
                     for (int s0 = 0; s0 < NS; s0 += 2 * PF) {
 #pragma unroll
                         for (int j = 0; j < PF; ++j)
-                            if (s0 + PF + j < NS) bB[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + PF + j, src, tb, c, colOk, same, Aimg);
+                            if (s0 + PF + j < NS) bB[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + PF + j, src, tb, c, colOk, same, Aimg, nfl);
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                         for (int j = 0; j < PF; ++j) {
@@ -476,7 +580,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                         if (s0 + PF < NS) {
 #pragma unroll
                             for (int j = 0; j < PF; ++j)
-                                if (s0 + 2 * PF + j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 2 * PF + j, src, tb, c, colOk, same, Aimg);
+                                if (s0 + 2 * PF + j < NS) bA[j] = fetchB<TC, GLOBAL_B>(bp, pu, sb + s0 + 2 * PF + j, src, tb, c, colOk, same, Aimg, nfl);
                             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                             for (int j = 0; j < PF; ++j) {
@@ -511,6 +615,26 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                 if (!g.parity) __syncthreads();
             }
         }
+        // outputs of this block whose real window holds a non-finite sample: the reference's values
+        bool fix = nfB;
+        if constexpr (GLOBAL_B) { fix = __syncthreads_or(nfl); nfl = false; }
+        if (fix) {
+            __syncthreads();  // every output of the block stored (vmcnt(0) + barrier) before it is overwritten
+            for (int cl = 0; cl < 16 * g.ncg; ++cl) {
+                const int colx = b * 16 * g.ncg + cl;
+                if (colx >= g.ncols) break;
+                const int lo = GLOBAL_B ? 0 : nfLo[it & 1][cl], hi = GLOBAL_B ? (1 << 30) : nfHi[it & 1][cl];
+                if (hi < 0) continue;
+                const int chx = colx / g.C;
+                bgNfFixRange<TC>(p, src, od, g.a_lo + static_cast<int64_t>(chx) * g.G, g.G, 0, g.Pc, colx - chx * g.C, lo, hi,
+                                 threadIdx.x, blockDim.x);
+            }
+            __syncthreads();  // this parity's ranges read by every wave
+            if (!GLOBAL_B) {
+                for (int i = threadIdx.x; i < 64; i += blockDim.x) { nfLo[it & 1][i] = 0x7fffffff; nfHi[it & 1][i] = -1; }
+                if (threadIdx.x == 0) nfFlag[it & 1] = 0;
+            }
+        }
     }
     if (g.hn > 0) {  // history keep for the next call (launchGather's job, folded into this launch)
         const int64_t total = g.hn * g.C;
@@ -533,7 +657,7 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
 // workgroups walking every row block.
 // History keep of a bg_rb_kernel launch (the `copy(history, history[consumed:])` of the stage):
 // element i of the new history is copied by thread i (mod the grid) of the flattened grid, issued right after the program's A / B loads so its memory round trip overlaps theirs.
-// Workgroup wg of nwg (the launch's grid, or the part of a pair launch running this stage).
+// Workgroup wg of nwg of the launch's grid.
 template <class TC>
 __device__ __forceinline__ void bgRbHistKeepW(const SrcDesc& src, const BgGrid& g, int wg, int nwg) {
     if (g.hn <= 0 || (g.dbg & 64)) return;
@@ -551,9 +675,39 @@ __device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g
 
 // One (column block, row block) item v of a bg_rb_kernel launch.  keep: this workgroup's share
 // (workgroup wg of nwg) of the history keep rides on this item.
+// Non-finite bookkeeping of the small launches, per wave (each wave writes only its own entries,
+// other waves read them between two barriers, the owner resets them after the item): bg_rb_kernel
+// keeps a row range per column of the item (rows relative to the column's a * Qc), bg_rt_kernel one
+// range (rows of the staged window).
+struct BgNfRb {
+    int lo[kBgRbMaxWaves][16], hi[kBgRbMaxWaves][16], any[kBgRbMaxWaves];
+};
+__device__ __forceinline__ void bgNfRbInit(BgNfRb& nf, int wt, int lane) {
+    if (lane < 16) { nf.lo[wt][lane] = 0x7fffffff; nf.hi[wt][lane] = -1; }
+    if (lane == 0) nf.any[wt] = 0;
+}
+
+// Item (column block b, row block rb) of bg_rb_kernel: its outputs whose real window meets a
+// recorded row range (waves < np) -- thread tid of nth.
+template <class TC>
+__device__ void bgRbFix(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int b, int rb, int np,
+                        const BgNfRb& nf, int tid, int nth) {
+    for (int idx = tid; idx < 256; idx += nth) {
+        const int n = idx & 15, r = rb * 16 + (idx >> 4);
+        const int col = b * 16 + n;
+        if (r >= g.Pc || col >= g.ncols) continue;
+        int lo = 0x7fffffff, hi = -1;
+        for (int w = 0; w < np; ++w) { lo = min(lo, nf.lo[w][n]); hi = max(hi, nf.hi[w][n]); }
+        if (hi < 0) continue;
+        const int w0 = p.xInfo[r], w1 = w0 + p.xInfo[p.Pc + r];
+        if (w1 <= lo || w0 > hi) continue;
+        bgNfFixOne<TC>(p, src, od, g.a_lo + col / g.C, r, col % g.C);
+    }
+}
+
 template <class TC, int NS>
 __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
-                                         typename Acc<TC>::V (*slots)[64], bool keep, int wg, int nwg) {
+                                         typename Acc<TC>::V (*slots)[64], bool keep, int wg, int nwg, BgNfRb& nf) {
     typedef typename Acc<TC>::V V;
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
@@ -615,20 +769,54 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
             else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
         }
         r = acc0 + acc1;
+        // non-finite B (checked beside the MFMA chain; rare): stage them as 0, record their rows, rerun
+        bool bad = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) bad |= !bgFinite(B[s]);
+        if (__builtin_expect(__any(bad), 0)) {
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                if (!bgFinite(B[s])) {
+                    B[s] = TC(0);
+                    atomicMin(&nf.lo[wt][lane & 15], k0 + 4 * s + (lane >> 4));
+                    atomicMax(&nf.hi[wt][lane & 15], k0 + 4 * s + (lane >> 4));
+                }
+            if (lane == 0) nf.any[wt] = 1;
+            acc0 = V{0, 0, 0, 0};
+            acc1 = acc0;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
+                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
+            }
+            r = acc0 + acc1;
+        }
         if (np > 1) slots[wt][lane] = r;
         if (kBgDev && stm.on) { __builtin_amdgcn_s_waitcnt(0); stm.mark(); }  // MFMA chain done
     }
     if (np > 1) {
         __syncthreads();
         stm.mark();  // reduction barrier
+        bool fix = false;  // a wave of this item staged a non-finite sample (uniform: read between barriers)
+        for (int w = 0; w < np; ++w) fix |= nf.any[w] != 0;
         if (wt == 0) {
             V sum = slots[0][lane];
             for (int k = 1; k < np; ++k) sum += slots[k][lane];
             if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
         }
-        __syncthreads();  // slots free for the next (column block, row block)
-    } else if (wt == 0 && !(g.dbg & 2)) {
-        storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        __syncthreads();  // slots free for the next (column block, row block); wave 0's stores done
+        if (fix) {
+            bgRbFix<TC>(p, src, od, g, b, rb, np, nf, threadIdx.x, blockDim.x);
+            __syncthreads();  // every wave read the ranges
+            if (wt < np && nf.any[wt]) bgNfRbInit(nf, wt, lane);
+        }
+    } else if (wt == 0) {
+        if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        if (nf.any[0]) {  // the item's only wave: fix its outputs itself, after its own stores
+            __builtin_amdgcn_s_waitcnt(0);
+            bgRbFix<TC>(p, src, od, g, b, rb, 1, nf, lane, 64);
+            bgNfRbInit(nf, 0, lane);
+        }
     }
     stm.done(g, 32);
 }
@@ -651,12 +839,14 @@ template <class TC, int NS>
 __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
     typedef typename Acc<TC>::V V;
     __shared__ V slots[kBgRbMaxWaves][64];
+    __shared__ BgNfRb nf;
+    bgNfRbInit(nf, threadIdx.x >> 6, threadIdx.x & 63);  // each wave its own entries (no barrier needed)
     const int64_t total = bgXcdSlots(g.nblocks, p.nrb);
     bool kept = false;
     for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {  // uniform per workgroup
         int b, rb;
         if (!bgXcdItem(bb, p.nrb, g.nblocks, b, rb)) continue;
-        bgRbItem<TC, NS>(p, src, od, g, b * p.nrb + rb, slots, !kept, blockIdx.x, gridDim.x);
+        bgRbItem<TC, NS>(p, src, od, g, b * p.nrb + rb, slots, !kept, blockIdx.x, gridDim.x, nf);
         kept = true;
     }
     if (!kept) bgRbHistKeep<TC>(src, g);  // a workgroup without an item
@@ -680,7 +870,7 @@ inline size_t bgRtLds(int Qc, int Kread, int nprog, size_t esz) {
 // One (row block, channel, chunk block) item v of a bg_rt_kernel launch (smem: the window + slots).
 template <class TC, int NS>
 __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
-                                         unsigned char* smem, bool keep, int wg, int nwg) {
+                                         unsigned char* smem, bool keep, int wg, int nwg, int* nfLo, int* nfHi) {
     typedef typename Acc<TC>::V V;
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
@@ -717,6 +907,10 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
 #pragma unroll
         for (int u = 0; u < kRtB; ++u) {
             const int r = r0 + u * blockDim.x;
+            if (__builtin_expect(!bgFinite(vv[u]), 0)) {  // staged as 0, its row recorded (bgNfFixOne)
+                vv[u] = TC(0);
+                if (r < nrow) { atomicMin(&nfLo[wt], r); atomicMax(&nfHi[wt], r); }
+            }
             if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
         }
     }
@@ -724,6 +918,8 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
     stm.mark();  // A issued, window staged by this wave
     __syncthreads();  // window staged
     stm.mark();
+    int nlo = 0x7fffffff, nhi = -1;  // rows of the window where non-finite samples were staged (uniform)
+    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) { nlo = min(nlo, nfLo[w]); nhi = max(nhi, nfHi[w]); }
     const int n = lane & 15, kq = lane >> 4;
     const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
     const bool colOk = 16 * kb + n < g.nchunk;
@@ -763,13 +959,21 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
     } else if (wt == 0 && !(g.dbg & 2)) {
         storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
     }
+    if (nhi >= 0) {  // outputs whose real window holds a non-finite sample: the reference's values
+        __syncthreads();  // the item's outputs stored
+        bgNfFixRange<TC>(p, src, od, g.a_lo + 16 * static_cast<int64_t>(kb), 16, rb * 16, min(rb * 16 + 16, g.Pc), c, nlo, nhi,
+                         threadIdx.x, blockDim.x);
+    }
     __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
+    if (nhi >= 0 && lane == 0) { nfLo[wt] = 0x7fffffff; nfHi[wt] = -1; }  // every wave read them before the barrier
     stm.done(g, 0);
 }
 
 template <class TC, int NS>
 __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int nfLo[kBgRbMaxWaves], nfHi[kBgRbMaxWaves];  // per wave: rows of non-finite samples staged
+    if ((threadIdx.x & 63) == 0) { nfLo[threadIdx.x >> 6] = 0x7fffffff; nfHi[threadIdx.x >> 6] = -1; }
     const int nkb = (g.nchunk + 15) / 16;
     const int M = p.nrb * g.C;  // items of one time block: row blocks x channels
     const int64_t total = bgXcdSlots(nkb, M);
@@ -778,167 +982,12 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
         int kb, m;
         if (!bgXcdItem(bb, M, nkb, kb, m)) continue;
         const int rb = m % p.nrb, c = m / p.nrb;
-        bgRtItem<TC, NS>(p, src, od, g, rb + p.nrb * (c * nkb + kb), smem, !kept, blockIdx.x, gridDim.x);
+        bgRtItem<TC, NS>(p, src, od, g, rb + p.nrb * (c * nkb + kb), smem, !kept, blockIdx.x, gridDim.x, nfLo, nfHi);
         kept = true;
     }
     // every thread of a workgroup with an item copied its share in its first item (no
     // second pass); a workgroup without one copies it here
     if (!kept) bgRbHistKeep<TC>(src, g);
-}
-
-// Small launches of row-block-aligned plans, column blocks as bg_rb_kernel (16 consecutive columns,
-// column = chunk * C + channel) but each workgroup stages its block's union window -- rows
-// [first chunk's window start, last chunk's window end) x the block's channels -- once in LDS,
-// row-major ([row][channel]), so the staging loads of an interleaved stream are contiguous
-// (GAR_BG_RT=2).  Same programs, same sums as bg_kernel / bg_rb_kernel.
-__host__ __device__ inline void bgRcGeom(int64_t C, int Qc, int Kread, int& rows, int& width) {
-    // the widest block: 16 columns spanning the most chunks (C < 16) or 16 channels (C >= 16)
-    const int64_t chunks = C >= 16 ? 2 : (15 + C - 1) / C + 1;
-    rows = static_cast<int>((chunks - 1) * Qc + Kread);
-    width = static_cast<int>(C >= 16 ? 16 : C);
-}
-inline size_t bgRcLds(int64_t C, int Qc, int Kread, int nprog, size_t esz) {
-    int rows, width;
-    bgRcGeom(C, Qc, Kread, rows, width);
-    return (static_cast<size_t>(rows) * (width + 1) * esz + 15) / 16 * 16 + static_cast<size_t>(nprog) * 64 * 4 * esz;
-}
-
-template <class TC, int NS>
-__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rc_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
-    typedef typename Acc<TC>::V V;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63;
-    const int wt = threadIdx.x >> 6;
-    const TC* Aimg = static_cast<const TC*>(p.A);
-    int rowsMax, width;
-    bgRcGeom(g.C, g.Qc, g.Wl, rowsMax, width);
-    const int ws = width + 1;  // padded row: the 16 columns of a B read spread over the banks
-    TC* win = reinterpret_cast<TC*>(smem);
-    V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(rowsMax) * ws * sizeof(TC) + 15) / 16 * 16);
-    const int nv = g.nblocks * p.nrb;
-    const bool same = srcSameType<TC>(src);
-    for (int v = blockIdx.x; v < nv; v += gridDim.x) {  // uniform per workgroup
-        const int b = v / p.nrb, rb = v - b * p.nrb;
-        const int ps = g.rbStart[rb], np = g.rbStart[rb + 1] - ps;
-        TC A[NS];
-        int k0 = 0;
-        if (wt < np) {  // A lands while the window is staged
-            const int pr = ps + wt;
-            k0 = g.rbK0[pr];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) A[s] = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
-        }
-        const int col0 = b * 16, kf = col0 / g.C;
-        const int c0 = g.C >= 16 ? col0 - kf * g.C : 0;  // first channel of the block (C >= 16), else 0
-        const int kl = min(col0 + 15, g.ncols - 1) / g.C;
-        const int nrow = (kl - kf) * g.Qc + g.Wl;
-        const int64_t T = (g.a_lo + kf) * g.Qc;
-        const int nel = nrow * width;
-        for (int e0 = threadIdx.x; e0 < nel; e0 += 4 * blockDim.x) {
-            TC vv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = e0 + u * blockDim.x;
-                const int r = e / width, ch = e - r * width;
-                const int c = c0 + ch;
-                const bool ok = e < nel && c < g.C;
-                vv[u] = same ? srcReadBF<TC>(src, T + r, ok ? c : 0, ok, Aimg) : (ok ? srcRead<TC>(src, T + r, c) : TC(0));
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int e = e0 + u * blockDim.x;
-                const int r = e / width, ch = e - r * width;
-                if (e < nel) win[r * ws + ch] = vv[u];
-            }
-        }
-        if (v == static_cast<int>(blockIdx.x)) bgRbHistKeep<TC>(src, g);  // its round trip beside the staging
-        __syncthreads();  // window staged
-        const int col = col0 + (lane & 15), kq = lane >> 4;
-        const bool colOk = col < g.ncols;
-        const int kc = colOk ? col / g.C : kf, c = colOk ? col - kc * g.C : c0;
-        const int64_t a = g.a_lo + kc;
-        V r = {0, 0, 0, 0};
-        if (wt < np) {
-            const int base = ((kc - kf) * g.Qc + k0 + kq) * ws + (c - c0);
-            TC B[NS];
-#pragma unroll
-            for (int s = 0; s < NS; ++s) B[s] = win[base + 4 * s * ws];
-            V acc0 = {0, 0, 0, 0}, acc1 = acc0;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
-                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
-            }
-            r = acc0 + acc1;
-            if (np > 1) slots[wt * 64 + lane] = r;
-        }
-        if (np > 1) {
-            __syncthreads();
-            if (wt == 0) {
-                V sum = slots[lane];
-                for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
-                if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
-            }
-        } else if (wt == 0 && !(g.dbg & 2)) {
-            storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
-        }
-        __syncthreads();  // window and slots free for the next (column block, row block)
-    }
-    // every thread of a workgroup with an item copied its share in the first iteration (ADVICE r04:
-    // no second pass); a workgroup without one copies it here
-    if (static_cast<int>(blockIdx.x) >= nv) bgRbHistKeep<TC>(src, g);
-}
-
-// ---- pair launch: a decimator stage and the next stage's composite FIR in ONE launch --------------
-// A streaming call of a multi-stage f64 pipeline (cfg5: decimator 96k -> 48k, then the DFT x2 +
-// polyphase composite 48k -> 44.1k, constant.go:308-337) was two dependent small launches; the
-// second waited out the first launch's tail and its own ramp (r04: 18.8 us per call for the
-// skeleton alone).  Here workgroups take tickets from a device counter: tickets [0, n0) are the
-// decimator's bg_rt items, [n0, n0 + n1) the composite's bg_rb items.  A ticket is only handed out
-// once every lower one has been, so every decimator item is running or done when a composite item
-// starts: no dispatch-order or co-residency assumption.  A composite item first waits until all n0
-// decimator items have published (agent-scope release / acquire through the second counter: the
-// decimated samples cross XCDs through L2 write-back), then runs exactly bg_rb_kernel's item --
-// the same programs, the same sums, the same bits.  Both counters only grow (unsigned wrap, signed
-// differences); the host keeps their values at launch (tick0, done0).
-struct BgPair {
-    BgDev p0, p1;
-    SrcDesc s0, s1;
-    OutDesc o0, o1;
-    BgGrid g0, g1;
-    unsigned* ctr;           // [0] tickets handed out, [1] decimator items published
-    unsigned tick0, done0;   // their values when this launch starts
-    int n0, n1;              // items of each stage
-    int* err;                // device status word: the hand-off wait expired (code kBgErrPairWait)
-};
-
-template <int NS0, int NS1>
-__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_pair_kernel(BgPair a) {
-    typedef typename Acc<double>::V V;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ V slots[kBgRbMaxWaves][64];
-    __shared__ int tk;
-    if (threadIdx.x == 0) tk = static_cast<int>(__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.tick0);
-    __syncthreads();
-    const int t = tk;
-    if (t < a.n0) {
-        bgRtItem<double, NS0>(a.p0, a.s0, a.o0, a.g0, t, smem, true, t, a.n0);
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed in L2
-        __syncthreads();                // ... and every other wave's
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (t < a.n0 + a.n1) {
-        if (threadIdx.x == 0) {
-            const unsigned want = a.done0 + static_cast<unsigned>(a.n0);
-            int it = 0;
-            for (; it < (1 << 22); ++it) {
-                if (static_cast<int>(__hip_atomic_load(a.ctr + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (it >= (1 << 22) && a.err) __hip_atomic_store(a.err, kBgErrPairWait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        __syncthreads();
-        bgRbItem<double, NS1>(a.p1, a.s1, a.o1, a.g1, t - a.n0, slots, true, t - a.n0, a.n1);
-    }
 }
 
 template <class TC, int NS>
@@ -955,9 +1004,6 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
             if (g.rbMode == 2) {  // time-major, LDS-staged windows
                 if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)); lim_ < lds) return ldsTooBig("bg_rt_kernel", lds, lim_);
                 hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
-            } else if (g.rbMode == 3) {  // column blocks, row-major LDS-staged windows
-                if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rc_kernel<TC, NS>)); lim_ < lds) return ldsTooBig("bg_rc_kernel", lds, lim_);
-                hipLaunchKernelGGL((bg_rc_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
             } else {
                 hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
             }

@@ -30,6 +30,7 @@
 #include "gar_design.hpp"
 #include "gar_kernels.hpp"
 #include "gar_plan.hpp"
+#include "gar_pool.hpp"
 
 namespace gar {
 namespace {
@@ -88,6 +89,7 @@ struct StageRT {
     FirPeriodic compositeFir;
     BgPlan fusedP, dftP, decimP;
     DevBuf fusedA, fusedT, dftA, dftT, decimA, decimT;
+    DevBuf fusedX, dftX, decimX, xBankA, xBankC;  // exact rows of the non-finite fixup (attachExact)
     BgDev fusedD{}, dftD{}, decimD{};
     DevBuf pa, pb, pc, pd, pabcd;
     PolyDev polyD{};
@@ -191,6 +193,28 @@ BgDev uploadPlan(const BgPlan& p, DevBuf& A, DevBuf& T, bool dry) {
     return d;
 }
 
+// Exact rows of a plan (non-finite fixup, BgDev::xRows): [rows | rowInfo] in one buffer; the
+// composite's two stages' banks are shared by the stage (xBankA / xBankC).
+void attachExact(const BgPlan& p, DevBuf& X, StageRT& s, BgDev& d, bool dry) {
+    d.xRowMax = p.rowMax;
+    d.xTwoStage = p.twoStage ? 1 : 0;
+    d.xT1 = s.d.dft.taps;
+    d.xT2 = s.d.poly.taps;
+    if (dry) return;
+    const size_t nr = p.rows.size(), ni = p.rowInfo.size();
+    X.ensure(nr * 8 + ni * 4 + 16);
+    HIPCHK(hipMemcpy(X.p, p.rows.data(), nr * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(static_cast<char*>(X.p) + nr * 8, p.rowInfo.data(), ni * 4, hipMemcpyHostToDevice));
+    d.xRows = static_cast<const double*>(X.p);
+    d.xInfo = reinterpret_cast<const int*>(static_cast<const char*>(X.p) + nr * 8);
+    if (p.twoStage) {
+        if (!s.xBankA.p) s.xBankA.upload(s.d.poly.a);
+        if (!s.xBankC.p) s.xBankC.upload(s.d.dft.c);
+        d.xPolyA = static_cast<const double*>(s.xBankA.p);
+        d.xDftC = static_cast<const double*>(s.xBankC.p);
+    }
+}
+
 template <class T>
 void uploadBank(const std::vector<double>& v, DevBuf& b) {
     std::vector<T> c(v.begin(), v.end());
@@ -205,17 +229,20 @@ bool buildStage(StageRT& s, bool f64, bool hx, bool dry, std::string& err) {
     if (d.kind == EngineKind::DftOnly || d.kind == EngineKind::DftPoly) {
         if (!buildBgPlan(firFromDft(d.dft), f64, s.dftP)) { err = "DFT plan"; return false; }
         s.dftD = uploadPlan(s.dftP, s.dftA, s.dftT, dry);
+        attachExact(s.dftP, s.dftX, s, s.dftD, dry);
         if (hx) attachHx(firFromDft(d.dft), s.dftH, s.dftD, dry, d);
     }
     if (d.kind == EngineKind::Decim) {
         if (!buildBgPlan(firFromDecim(d.decim), f64, s.decimP)) { err = "decimator plan"; return false; }
         s.decimD = uploadPlan(s.decimP, s.decimA, s.decimT, dry);
+        attachExact(s.decimP, s.decimX, s, s.decimD, dry);
         if (hx) attachHx(firFromDecim(d.decim), s.decimH, s.decimD, dry, d);
     }
     if (d.kind == EngineKind::DftPoly) {
         if (firComposite(d.dft, d.poly, s.compositeFir) && buildBgPlan(s.compositeFir, f64, s.fusedP)) {
             s.fused = true;
             s.fusedD = uploadPlan(s.fusedP, s.fusedA, s.fusedT, dry);
+            attachExact(s.fusedP, s.fusedX, s, s.fusedD, dry);
             if (hx) attachHx(s.compositeFir, s.fusedH, s.fusedD, dry, d);
         }
         PolyDev& p = s.polyD;
@@ -500,105 +527,6 @@ struct HostBuf {
     }
 };
 
-// Host worker pool for packing / unpacking large host C-ABI calls (one job split over
-// min(15, cores - 1) workers + the caller); small calls run inline.  Workers spin for ~100 us
-// after a job before sleeping (a streaming host call hands the pool two jobs, pack and unpack, a few
-// hundred microseconds apart; a futex wake per job and worker cost tens of microseconds), and job
-// completion is an atomic count.
-class Pool {
-   public:
-    static Pool& get() {
-        static Pool p;
-        return p;
-    }
-    void run(int n, const std::function<void(int)>& f) {
-        // one job at a time: handles are independent, so a second thread's call must not
-        // overwrite a running job; when the pool is busy that caller runs its job inline
-        std::unique_lock<std::mutex> owner(runMu_, std::try_to_lock);
-        if (n <= 1 || th_.empty() || !owner.owns_lock()) {
-            for (int i = 0; i < n; ++i) f(i);
-            return;
-        }
-        uint64_t g;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            job_.store(&f);
-            njobs_.store(n);
-            pending_.store(n);
-            g = (ticket_.load() >> 32) + 1;
-            ticket_.store(g << 32);  // publishes the job: generation g, next index 0
-            cv_.notify_all();
-        }
-        work(g);
-        if (!spinUntil([&] { return pending_.load() == 0; })) {
-            std::unique_lock<std::mutex> lk(mu_);
-            done_.wait(lk, [&] { return pending_.load() == 0; });
-        }
-    }
-    int workers() const { return static_cast<int>(th_.size()) + 1; }
-
-   private:
-    Pool() {
-        const unsigned hw = std::thread::hardware_concurrency();
-        const int n = std::max(0, std::min<int>(15, static_cast<int>(hw) - 1));
-        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
-    }
-    ~Pool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_.store(true);
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    template <class P>
-    static bool spinUntil(P pred) {  // up to ~100 us
-        const auto t0 = std::chrono::steady_clock::now();
-        for (int k = 0;; ++k) {
-            if (pred()) return true;
-            _mm_pause();
-            if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) return false;
-        }
-    }
-    // Claims indices of generation g only (a worker that woke late for a finished job must not
-    // take an index of the next one: compare-and-swap on the (generation, index) ticket).
-    void work(uint64_t g) {
-        for (;;) {
-            uint64_t t = ticket_.load();
-            for (;;) {
-                if ((t >> 32) != g || static_cast<int64_t>(t & 0xffffffffu) >= njobs_.load()) return;
-                if (ticket_.compare_exchange_weak(t, t + 1)) break;
-            }
-            (*job_.load())(static_cast<int>(t & 0xffffffffu));
-            if (pending_.fetch_sub(1) == 1) {
-                std::lock_guard<std::mutex> lk(mu_);
-                done_.notify_all();
-            }
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            if (!spinUntil([&] { return stop_.load() || (ticket_.load() >> 32) != seen; })) {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_.load() || (ticket_.load() >> 32) != seen; });
-            }
-            if (stop_.load()) return;
-            seen = ticket_.load() >> 32;
-            work(seen);
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex runMu_;  // held by the caller whose job the workers run
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    std::atomic<const std::function<void(int)>*> job_{nullptr};
-    std::atomic<int> njobs_{0};
-    std::atomic<int> pending_{0};
-    std::atomic<uint64_t> ticket_{0};  // generation << 32 | next job index
-    std::atomic<bool> stop_{false};
-};
-
 // Runs f(c, lo, hi) over channels x [0, n) samples: inline below ~1 MiB of data, else split over
 // the pool -- whole channels per job when there are many channels (2 jobs per worker), else
 // slices of channels.
@@ -673,7 +601,6 @@ struct gar_resampler {
     // (hxt_kernel: an expired progress wait) writes a nonzero code; every ABI call checks it first
     int* errHost = nullptr;
     int* errDev = nullptr;
-    gar::BgPairCtr pairCtr;  // device counters of decimator + composite pair launches
     gar_config cfg{};
     std::vector<std::unique_ptr<gar::StageRT>> stages;
     std::vector<gar::Group> groups;
@@ -706,40 +633,16 @@ void trimHost(Handle* h) {
     if (h->hostOut.cap > kPinKeep) h->hostOut.release();
 }
 
-// A decimator launch held back so that the next stage's composite launch can take it along
-// (launchBgPair: one launch per streaming call of a decimator -> DFT x2 + polyphase pipeline).
-struct PendingBg {
-    bool on = false;
-    const BgDev* p = nullptr;
-    SrcDesc src{};
-    OutDesc od{};
-    int C = 0;
-    HistCopy hc;
-};
-
 struct Ctx {
     Handle* h;
     Group* g;
     hipStream_t s;
     bool launch;
-    PendingBg* pend = nullptr;  // set for real launches (not the counting passes)
-    bool deferNext = false;     // the next decimator launch may wait for its partner
 };
 
-template <class L>
-hipError_t timedRaw(Ctx& x, int tag, L&& launch);
-void flushPending(Ctx& x);
-
 // A launch bracketed by HIP events on its stream when profiling is on (tag = gar_profile_read kind).
-// Any held-back decimator launch goes first (stream order = the stages' order).
 template <class L>
 hipError_t timed(Ctx& x, int tag, L&& launch) {
-    flushPending(x);
-    return timedRaw(x, tag, launch);
-}
-
-template <class L>
-hipError_t timedRaw(Ctx& x, int tag, L&& launch) {
     if (!x.h->profile || !((x.h->profileKinds >> tag) & 1u)) return launch();
     hipEvent_t a, b;
     if (!x.h->evPool.empty()) {  // reuse event pairs (creation is not free)
@@ -759,46 +662,8 @@ hipError_t timedRaw(Ctx& x, int tag, L&& launch) {
     return e;
 }
 
-// Launches a held-back decimator on its own (its partner did not come, or cannot pair).
-void flushPending(Ctx& x) {
-    if (!x.pend || !x.pend->on) return;
-    PendingBg& d = *x.pend;
-    d.on = false;
-    HistCopy hc = d.hc;
-    hc.done = false;
-    HIPCHK(timedRaw(x, 2, [&] { return launchBg(*d.p, d.src, d.od, d.C, x.s, &hc); }));
-    // the keep was promised to the stage's bookkeeping when the launch was held back
-    if (hc.n > 0 && hc.dst && !hc.done)
-        HIPCHK(launchGather(1, d.src, hc.dst, hc.t0, hc.n, d.C, x.s));
-}
-
 hipError_t timedBg(Ctx& x, int tag, const BgDev& p, const SrcDesc& src, const OutDesc& od, int C,
                    HistCopy* hc = nullptr) {
-    if (x.deferNext && x.pend && tag == 2 && p.f64 && !x.pend->on) {  // hold the decimator back for its partner
-        x.deferNext = false;
-        PendingBg& d = *x.pend;
-        d.on = true;
-        d.p = &p;
-        d.src = src;
-        d.od = od;
-        d.C = C;
-        d.hc = hc ? *hc : HistCopy();
-        if (hc && hc->n > 0 && hc->dst) hc->done = true;  // taken by the pair launch or by flushPending
-        return hipSuccess;
-    }
-    if (x.pend && x.pend->on && tag == 0 && p.f64) {  // the composite of the same call: one launch for both
-        PendingBg& d = *x.pend;
-        HistCopy h0 = d.hc;
-        h0.done = false;
-        const hipError_t e = timedRaw(x, 0, [&] {
-            return launchBgPair(*d.p, d.src, d.od, &h0, p, src, od, hc, C, x.s, x.h->pairCtr);
-        });
-        if (e != hipErrorNotSupported) {
-            d.on = false;
-            if (e == hipSuccess && h0.n > 0 && h0.dst && !h0.done) throw DevError{hipErrorUnknown, "pair launch left the decimator's history keep"};
-            return e;
-        }
-    }
     return timed(x, tag, [&] { return launchBg(p, src, od, C, x.s, hc); });
 }
 
@@ -842,7 +707,6 @@ void hist_update(Ctx& x, Hist& hs, const SrcDesc& src, int64_t k0, int64_t k1) {
     if (!x.launch) { hs.base = k0; hs.len = k1 - k0; hs.zero = false; return; }
     const int other = 1 - hs.cur;
     hs.buf[other].ensure(static_cast<size_t>(std::max<int64_t>(k1 - k0, 1)) * C * tc);
-    flushPending(x);
     HIPCHK(launchGather(x.h->f64, src, hs.buf[other].p, k0, k1 - k0, C, x.s));
     hs.cur = other;
     hs.base = k0;
@@ -934,7 +798,6 @@ int64_t stageProcess(Ctx& x, int si, const InView& in, const OutView& out) {
         }
         case EngineKind::Passthrough: {
             if (x.launch && !in.zeros) {
-                flushPending(x);
                 HIPCHK(launchCopy(in.p, in.f64, in.fs, in.cs, out.p, out.f64, out.fs, out.cs, n, C, x.s));
             }
             c.y_count += n;
@@ -1124,26 +987,12 @@ int64_t chainProcess(Ctx& x, const InView& in, const OutView& out, std::vector<i
             }
         }
         int64_t m = 0;
-        // decimator -> fused DFT x2 + polyphase (f64): the two launches of a call as one (launchBgPair)
-        // when GAR_BG_PAIR=1 (read per call).  Off by default: measured slower than the two launches
-        // (cfg5 4800-frame calls 37.3 vs 30.4 us of kernel time, profiles/r05b_cfg5_pair.txt) -- the
-        // agent-scope hand-off inside the launch (L2 write-back + invalidate, ~4-8 us) costs more than
-        // the launch boundary it replaces.
-        const char* pk = i + 1 < ns ? std::getenv("GAR_BG_PAIR") : nullptr;
-        const bool pairOn = pk && pk[0] == '1';
-        x.deferNext = pairOn && x.launch && x.pend && !last && x.h->f64 && x.h->stages[i]->d.kind == EngineKind::Decim &&
-                      x.h->stages[i + 1]->d.kind == EngineKind::DftPoly && x.h->stages[i + 1]->fused &&
-                      !x.g->cnt[i + 1].staged;
-        const bool held = x.pend && x.pend->on;  // stage i - 1's decimator waits for this stage
         if (cur.n >= 1) m = stageProcess(x, i, cur, o);  // Available() >= GetMinInput() (constant.go:277,314)
-        x.deferNext = false;
-        if (held && x.pend->on) flushPending(x);  // this stage launched nothing to pair with
         sizes[i] = m;
         InView nx;
         nx.p = o.p; nx.fs = o.fs; nx.cs = o.cs; nx.f64 = o.f64; nx.n = m;
         cur = nx;
     }
-    flushPending(x);
     return cur.n;
 }
 
@@ -1279,8 +1128,7 @@ int64_t runGroup(Handle* h, Group& g, const InView& in, const OutView& out, bool
         return n;
     }
     h->scratchSizes = sizes;
-    PendingBg pend;
-    Ctx x{h, &g, s, true, &pend};
+    Ctx x{h, &g, s, true};
     std::vector<int64_t> s2;
     const int64_t got = flush ? chainFlush(x, out, s2) : chainProcess(x, in, out, s2);
     if (got != n) { st = GAR_ERR_INTERNAL; g_err = "size mismatch between count and launch"; }
@@ -1342,7 +1190,6 @@ bool devFault(Handle* h) {
     h->poisoned = true;
     const char* what = v == kHxtErrLoadWait   ? "hxt_kernel: a compute wave's LDS load-progress wait expired"
                        : v == kHxtErrSlotWait ? "hxt_kernel: a loader's LDS ring-slot wait expired"
-                       : v == kBgErrPairWait  ? "bg_pair_kernel: a composite item's wait for the decimator items expired"
                                               : "unknown code";
     g_err = std::string("device error reported by ") + what + " (code " + std::to_string(v) +
             "); outputs of the launch are invalid; call Reset";
@@ -1468,10 +1315,6 @@ gar_status initDevice(Handle* h) {
     void* d = nullptr;
     HIPCHK(hipHostGetDevicePointer(&d, w, 0));
     h->errDev = static_cast<int*>(d);
-    void* pc = nullptr;
-    HIPCHK(hipMalloc(&pc, 2 * sizeof(unsigned)));
-    HIPCHK(hipMemset(pc, 0, 2 * sizeof(unsigned)));
-    h->pairCtr.dev = static_cast<unsigned*>(pc);
     return GAR_OK;
 }
 
@@ -1781,7 +1624,6 @@ void gar_free(gar_resampler* r) {
         r->groups.clear();
         r->stages.clear();
         if (r->failEv) (void)hipEventDestroy(r->failEv);
-        if (r->pairCtr.dev) (void)hipFree(r->pairCtr.dev);
         if (r->errHost) (void)hipHostFree(r->errHost);
         if (r->stream) (void)hipStreamDestroy(r->stream);
     } catch (...) {
@@ -2123,7 +1965,6 @@ void gar_reset(gar_resampler* r) {
             drainOrder(r);
             (void)hipGetLastError();
             if (r->errHost) __atomic_store_n(r->errHost, 0, __ATOMIC_RELEASE);  // every launch that could write it has drained
-            if (r->pairCtr.dev && hipMemset(r->pairCtr.dev, 0, 2 * sizeof(unsigned)) == hipSuccess) r->pairCtr.tick = r->pairCtr.done = 0;
             r->groups.clear();
             r->groups.push_back(freshGroup(r, 0, r->channels));
             r->poisoned = false;
@@ -2247,17 +2088,21 @@ void gar_profile_enable(gar_resampler* r, int32_t on) {
 int64_t gar_dev_pool_selftest(int32_t threads, int32_t iters, int32_t channels, int64_t frames) {
     if (threads < 1 || iters < 0 || channels < 1 || frames < 0) return -1;
     std::atomic<int64_t> bad{0};
+    // thread t uses channels + t channels, so consecutive jobs on the pool have different job
+    // counts (whole-channel jobs for C >= 2 * workers, channel slices below) -- the case where a
+    // stale ticket could claim an index of the next job
     auto body = [&](int t) {
-        std::vector<double> src(static_cast<size_t>(channels) * frames), dst(src.size());
+        const int channels_t = channels + t;
+        std::vector<double> src(static_cast<size_t>(channels_t) * frames), dst(src.size());
         std::vector<float> mid(src.size());
         for (size_t i = 0; i < src.size(); ++i) src[i] = static_cast<double>((i * 2654435761u + t) % 65536) / 65536.0 - 0.5;
         for (int k = 0; k < iters; ++k) {
             std::fill(dst.begin(), dst.end(), -9.0);
-            gar::forSlices(channels, frames, 12, [&](int c, int64_t lo, int64_t hi) {
+            gar::forSlices(channels_t, frames, 12, [&](int c, int64_t lo, int64_t hi) {
                 gar::packChannel<double>(mid.data() + static_cast<size_t>(c) * frames, false,
                                          src.data() + static_cast<size_t>(c) * frames, lo, hi);
             });
-            gar::forSlices(channels, frames, 12, [&](int c, int64_t lo, int64_t hi) {
+            gar::forSlices(channels_t, frames, 12, [&](int c, int64_t lo, int64_t hi) {
                 gar::unpackChannel<double>(dst.data() + static_cast<size_t>(c) * frames, false,
                                            mid.data() + static_cast<size_t>(c) * frames, lo, hi);
             });

@@ -68,7 +68,7 @@ hipError_t bgLaunchF32b(int NS, const BgDev& p, const SrcDesc& src, const OutDes
                         size_t lds, int64_t blocks, hipStream_t st, bool globalB);
 
 // Small-launch geometry of a row-block-aligned f64 plan (stream chunks): returns the launch mode
-// (0 not a small launch; 1 bg_rb_kernel, 2 bg_rt_kernel, 3 bg_rc_kernel) with g, the dynamic LDS and
+// (0 not a small launch; 1 bg_rb_kernel, 2 bg_rt_kernel) with g, the dynamic LDS and
 // the grid filled in.  The history keep hc is taken (hc->done) when the mode is not 0.
 // development: GAR_BG_PROF=1 (with a -DGAR_BG_DEV=1 build of the f64 units) sums the small
 // launches' phase stamps and prints them at exit
@@ -156,13 +156,6 @@ static int bgSmallGrid(const BgDev& p, const OutDesc& od, int C, HistCopy* hc, i
         lds = rtLds;
         return 2;
     }
-    const size_t rcLds = bgRcLds(C, p.Qc, p.Kread, p.maxPrb, 8);
-    if (knobRt == 2 && rcLds <= 160 * 1024 - 1024) {
-        g.rbMode = 3;
-        blocks = std::min<int64_t>(static_cast<int64_t>(g.nblocks) * p.nrb, 65535);
-        lds = rcLds;
-        return 3;
-    }
     blocks = std::min<int64_t>(bgXcdSlots(g.nblocks, p.nrb), 65528);  // XCD-grouped slots
     lds = 0;
     return 1;
@@ -172,52 +165,6 @@ static int numCUs() {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     return ncu;
-}
-
-// bg_pair_kernel instantiations (gar_bg_pair_*.hip): NS of the decimator's and the composite's programs
-hipError_t bgPairDispatch1(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
-hipError_t bgPairDispatch2(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
-hipError_t bgPairDispatch3(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st);
-static hipError_t bgPairDispatch(int NS0, int NS1, const BgPair& a, size_t lds, int64_t blocks, int threads, hipStream_t st) {
-    if (NS0 <= 16) return bgPairDispatch1(NS0, NS1, a, lds, blocks, threads, st);
-    if (NS0 <= 28) return bgPairDispatch2(NS0, NS1, a, lds, blocks, threads, st);
-    return bgPairDispatch3(NS0, NS1, a, lds, blocks, threads, st);
-}
-
-hipError_t launchBgPair(const BgDev& p0, const SrcDesc& s0, const OutDesc& o0, HistCopy* h0, const BgDev& p1,
-                        const SrcDesc& s1, const OutDesc& o1, HistCopy* h1, int C, hipStream_t stream, BgPairCtr& ctr) {
-    if (!ctr.dev || !p0.f64 || !p1.f64 || o0.o_hi <= o0.o_lo || o1.o_hi <= o1.o_lo) return hipErrorNotSupported;
-    const int ncu = numCUs();
-    BgPair a{};
-    HistCopy t0 = h0 ? *h0 : HistCopy(), t1 = h1 ? *h1 : HistCopy();
-    t0.done = t1.done = false;
-    size_t lds0 = 0, lds1 = 0;
-    int64_t b0 = 0, b1 = 0;
-    if (bgSmallGrid(p0, o0, C, &t0, ncu, a.g0, lds0, b0) != 2) return hipErrorNotSupported;  // decimator: bg_rt items
-    if (bgSmallGrid(p1, o1, C, &t1, ncu, a.g1, lds1, b1) != 1) return hipErrorNotSupported;  // composite: bg_rb items
-    const int64_t n0 = (a.g0.nchunk + 15) / 16 * static_cast<int64_t>(C) * p0.nrb;
-    const int64_t n1 = static_cast<int64_t>(a.g1.nblocks) * p1.nrb;
-    (void)b0;
-    (void)b1;
-    if (n0 + n1 > 65535) return hipErrorNotSupported;  // one item per workgroup
-    a.p0 = p0; a.p1 = p1;
-    a.s0 = s0; a.s1 = s1;
-    a.o0 = o0; a.o1 = o1;
-    a.ctr = ctr.dev;
-    a.tick0 = ctr.tick;
-    a.done0 = ctr.done;
-    a.n0 = static_cast<int>(n0);
-    a.n1 = static_cast<int>(n1);
-    a.err = o1.err;
-    const int threads = 64 * std::max(p0.maxPrb, p1.maxPrb);
-    const hipError_t e = bgPairDispatch(p0.NS, p1.NS, a, lds0, n0 + n1, threads, stream);
-    if (e == hipSuccess) {
-        ctr.tick += static_cast<unsigned>(n0 + n1);
-        ctr.done += static_cast<unsigned>(n0);
-        if (h0) h0->done = t0.done;
-        if (h1) h1->done = t1.done;
-    }
-    return e;
 }
 
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C, hipStream_t stream, HistCopy* hc) {
@@ -258,7 +205,7 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
     const int rowsPerPiece = p.f64 ? 2 : 4;
     auto wsFor = [&](int W) { return (W + rowsPerPiece - 1) / rowsPerPiece * rowsPerPiece; };
     auto tileBytes = [&](int G) { return 2 * static_cast<size_t>(tileN) * wsFor(p.Kread + (G - 1) * p.Qc) * sz; };
-    const size_t kLds = 160 * 1024;
+    const size_t kLds = 160 * 1024 - kBgStaticLds;  // bg_kernel's static LDS: the non-finite ranges
     g.parity = (g.nred > 0 && !knobNoParity && tileBytes(std::min<int64_t>(4, std::max<int64_t>(nmac, 1))) + 2 * slotBytes <= kLds) ? 1 : 0;
     const size_t partBytes = (g.parity ? 2 : 1) * slotBytes;
     int G = 1;

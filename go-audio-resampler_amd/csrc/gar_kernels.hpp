@@ -57,8 +57,6 @@ struct HxDev;
 // hxt_kernel (gar_hxt.hpp hxtWait) -- 1 a compute wave's load-progress wait expired, 2 a loader's
 // ring-slot wait expired.
 constexpr int kHxtErrLoadWait = 1, kHxtErrSlotWait = 2;
-// bg_pair_kernel (gar_bg.hpp): 3 a composite item's wait for the decimator items expired.
-constexpr int kBgErrPairWait = 3;
 
 // A launch whose configuration the device cannot run (dynamic LDS above the kernel's limit): the
 // launcher records what was exceeded here and returns hipErrorInvalidConfiguration; the C-ABI turns
@@ -80,6 +78,14 @@ struct BgDev {
     const int* rbStart; // [nrb + 1]
     const int* hRbStart; // host copies (bg_rb_kernel passes them by value): [nrb + 1]
     const int* hRbK0;    // first input row of each program [nprog]
+    // exact recompute of outputs whose real window holds a non-finite sample (gar_bg.hpp bgNfFixOne):
+    // the macro period's f64 rows and, for DFT x2 (*) polyphase composites, each row's polyphase
+    // phase / DFT parity and the two stages' banks (the reference's two-stage order)
+    const double* xRows;   // [Pc][xRowMax]
+    const int* xInfo;      // [4][Pc]: window offset, length, polyphase phase, DFT parity
+    int xRowMax, xTwoStage, xT1, xT2;
+    const double* xPolyA;  // [L][T2]
+    const double* xDftC;   // [2][T1]
 };
 
 // Device copy of an HxPlan (gar_plan.hpp): split-f16 MFMA FIR, f32 compute.
@@ -139,18 +145,6 @@ struct HistCopy {
 
 hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
                     HistCopy* hc = nullptr);
-// Device counters of pair launches (one per handle): tickets and published decimator items, and
-// their values the host expects at the next launch.
-struct BgPairCtr {
-    unsigned* dev = nullptr;  // [2]
-    unsigned tick = 0, done = 0;
-};
-// One streaming call's decimator stage (p0: its small launch would be bg_rt_kernel) and the next
-// stage's composite FIR (p1: bg_rb_kernel) as one launch (bg_pair_kernel); both history keeps ride
-// along.  hipErrorNotSupported when either launch is not of that shape (the caller launches them
-// one after the other).
-hipError_t launchBgPair(const BgDev& p0, const SrcDesc& s0, const OutDesc& o0, HistCopy* h0, const BgDev& p1,
-                        const SrcDesc& s1, const OutDesc& o1, HistCopy* h1, int C, hipStream_t stream, BgPairCtr& ctr);
 hipError_t launchHx(const HxDev& p, const SrcDesc& src, const OutDesc& out, int C, hipStream_t stream,
                     HistCopy* hc = nullptr);
 // True when a row-block plan fits launchHxs's geometry at one period per group (its smallest

@@ -347,6 +347,24 @@ bool buildBgPlan(const FirPeriodic& f, bool f64, BgPlan& plan) {
     if (f64) plan.A64 = std::move(A);
     else plan.A32.assign(A.begin(), A.end());
 
+    plan.rowMax = 0;
+    for (const auto& r : f.rows) plan.rowMax = std::max(plan.rowMax, static_cast<int>(r.size()));
+    plan.twoStage = f.composite;
+    plan.rows.assign(static_cast<size_t>(plan.Pc) * plan.rowMax, 0.0);
+    plan.rowInfo.assign(4 * static_cast<size_t>(plan.Pc), 0);
+    for (int r = 0; r < plan.Pc; ++r) {
+        int64_t off;
+        const std::vector<double>* row;
+        macroRow(f, r, off, row);
+        plan.rowInfo[r] = static_cast<int>(off);
+        plan.rowInfo[plan.Pc + r] = static_cast<int>(row->size());
+        if (f.composite) {
+            plan.rowInfo[2 * plan.Pc + r] = f.ph[r % f.P];
+            plan.rowInfo[3 * plan.Pc + r] = f.par[r % f.P];
+        }
+        std::copy(row->begin(), row->end(), plan.rows.begin() + static_cast<size_t>(r) * plan.rowMax);
+    }
+
     double useful = 0;
     for (const auto& r : f.rows) useful += static_cast<double>(r.size());
     plan.usefulMacsPerOutput = useful / f.P;

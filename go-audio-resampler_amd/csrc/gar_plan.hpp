@@ -79,6 +79,12 @@ struct BgPlan {
     std::vector<int> rbK0;            // first input row of each program (one segment each)
     std::vector<float> A32;           // [nw][kch*NS][64] MFMA A fragments
     std::vector<double> A64;
+    // exact rows of the macro period (non-finite fixup, BgDev::xRows): f64 rows [Pc][rowMax] and
+    // [offset | length | polyphase phase | DFT parity] per row (phase / parity of composite rows)
+    int rowMax = 0;
+    bool twoStage = false;
+    std::vector<double> rows;
+    std::vector<int> rowInfo;
     double usefulMacsPerOutput = 0;   // sum of row lengths / P
     double mfmaMacsPerOutput = 0;     // MFMA MACs / output over the band (excl. bucket padding)
     std::vector<int> progTable() const;  // [nprog][kBgProgInts]

@@ -398,3 +398,20 @@ def test_host_staging_pool_selftest(gar):
     assert f(3, 10, 3, 100000) == 0     # few channels: slices of channels
     assert f(8, 5, 256, 4096) == 0      # more caller threads than one job: the rest run inline
     assert f(2, 50, 2, 70000) == 0      # short jobs back to back: workers woken while spinning
+    # caller t uses channels + t: the threads' job counts differ and cross 2 * workers (whole-channel
+    # jobs vs channel slices), so consecutive jobs on the pool have different job counts
+    assert f(6, 20, 12, 20000) == 0
+    assert f(6, 20, 28, 12000) == 0
+
+
+def test_host_pool_tsan():
+    """ThreadSanitizer stress of the pool (tools/pool_tsan.cpp: callers with different job counts back
+    to back, every index exactly once, nothing running after run() returns)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "go-audio-resampler_amd")
+    r = subprocess.run(["make", "-s", "-C", root, "tsan"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 bad" in r.stdout

@@ -109,7 +109,7 @@ def _run_bench(nproc, extra):
     env = dict(os.environ)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    args = ["--dry-run", "--steps", "2", "--warmup", "1"] + extra
+    args = ["--dry-run", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"] + extra
     if nproc == 1:
         cmd = [sys.executable, os.path.join(root, "bench.py")] + args
     else:
@@ -158,7 +158,7 @@ def test_bench_gpus_flag_starts_ranks_itself():
     512 streams per rank, both ranks listed (VERDICT r04 'make --gpus authoritative')."""
     import json
     p = _bench_cmd(["--dry-run", "--gpus", "2", "--workload", "cfg4", "--seconds", "0.5", "--secondary", "none",
-                    "--steps", "2", "--warmup", "1"])
+                    "--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
@@ -168,6 +168,23 @@ def test_bench_gpus_flag_starts_ranks_itself():
     assert sorted(r["rank"] for r in d["ranks"]) == [0, 1]
     assert d["input_samples_total"] == 1024 * 2 * 22050
     assert list(d)[:4] == ["metric", "value", "unit", "n_gpus"]
+
+
+def test_bench_two_ranks_line_carries_cpu_baseline_and_per_rank():
+    """A world-2 line is as complete as a world-1 line: rank 0 times the CPU
+    baseline after the timed regions (here a bounded 0.3 s sample), and the line lists every rank's
+    own step time and kernel figures (all_gather over the process group)."""
+    import json
+    p = _bench_cmd(["--dry-run", "--gpus", "2", "--workload", "cfg2", "--seconds", "0.5", "--secondary", "cfg4",
+                    "--steps", "2", "--warmup", "1", "--cpu-baseline-seconds", "0.3"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["n_gpus"] == 2
+    cb = d["cpu_baseline"]
+    assert cb and cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    assert sorted(r["rank"] for r in d["per_rank"]) == [0, 1]
+    assert all(r["local_ms_per_step"] is not None for r in d["per_rank"])
+    assert sorted(r["rank"] for r in d["secondary"]["cfg4"]["per_rank"]) == [0, 1]
 
 
 def test_bench_gpus_flag_conflicts_with_world_size():

@@ -136,39 +136,3 @@ def test_cfg5_full_8ch_f64_60s_chunked(gar, O, cuda):
     want = oracle_new(O, 96000, 44100, x[:, 3:4], O.P_VERYHIGH, chunks=chunk_sizes(frames, 4800))[0]
     assert len(want) == y.shape[0]
     assert rms(y[:, 3], want) <= F64_RMS_TOL
-
-
-def test_cfg5_pair_launch_one_per_call(gar, O, cuda, monkeypatch):
-    """GAR_BG_PAIR=1: cfg5 streaming calls (decimator -> DFT x2 + polyphase, f64, 4800-frame chunks) go
-    out as ONE launch per call (bg_pair_kernel: the decimator's items, then the composite's after a
-    device hand-off): no separate decimator launch is profiled, every output equals
-    the one-shot call bit for bit (the same programs and sums as the two launches), and the oracle's
-    at the f64 bar.  Ragged chunk sizes included."""
-    monkeypatch.setenv("GAR_BG_PAIR", "1")  # opt-in path (measured slower than two launches by default)
-    frames = 96000 * 2 + 777
-    x = signal(frames, 8, 96000, seed=55)
-    xd = cuda.from_numpy(x).cuda()
-    one = gar.New(gar.Config(96000, 44100, 8, gar.QualityVeryHigh, ComputeDtype=gar.F64))
-    y1 = cuda.cat([one.process_device(xd).clone(), one.flush_device(dtype=cuda.float64).clone()])
-    r = gar.New(gar.Config(96000, 44100, 8, gar.QualityVeryHigh, ComputeDtype=gar.F64))
-    sizes = [4800] * 38 + [1, 4799, 2500, 3077]  # ragged tail: a one-frame call, odd sizes
-    assert sum(sizes) == frames
-    r.profile(True)
-    outs, s = [], 0
-    for n in sizes:
-        outs.append(r.process_device(xd[s:s + n]).clone())
-        s += n
-    cuda.cuda.synchronize()
-    _, dec_launches = r.profile_read(2)
-    _, fused_launches = r.profile_read(0)
-    r.profile(False)
-    outs.append(r.flush_device(dtype=cuda.float64).clone())  # (the flush chain launches stage by stage)
-    y = cuda.cat(outs)
-    # one launch per call: the decimator rides in the composite's launch; it runs alone only on a call
-    # whose composite stage emits nothing (here possibly the one-frame call)
-    assert dec_launches <= 1
-    assert fused_launches + dec_launches <= len(sizes)
-    assert fused_launches >= len(sizes) - 2
-    assert y.shape == y1.shape and cuda.equal(y, y1)
-    want = oracle_new(O, 96000, 44100, x[:, 5:6], O.P_VERYHIGH, chunks=sizes)[0]
-    assert rms(y[:, 5].cpu().numpy(), want) <= F64_RMS_TOL

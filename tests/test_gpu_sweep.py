@@ -471,13 +471,46 @@ def _loud_cases(n=30, seed=6060):
 LOUD = _loud_cases()
 
 
+def _nf_sets(a):
+    """(NaN, +Inf, -Inf) masks: the reference's non-finite outputs, class by class."""
+    a = np.asarray(a)
+    return np.isnan(a), np.isposinf(a), np.isneginf(a)
+
+
+def _run_stream(gar, ir, orr, ch, preset, dtype, x, ck):
+    """New(config) on the device API over x (frames x ch) in calls of ck frames (None: one call) + Flush."""
+    import torch
+    f64 = dtype == gar.F64
+    tdt = torch.float64 if f64 else torch.float32
+    r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=dtype))
+    xd = torch.from_numpy(np.ascontiguousarray(x)).to(tdt).cuda()
+    parts, s = [], 0
+    for n in (chunk_sizes(x.shape[0], ck) if ck else [x.shape[0]]):
+        parts.append(r.process_device(xd[s:s + n]).clone())
+        s += n
+    parts.append(r.flush_device(dtype=tdt).clone())
+    torch.cuda.synchronize()
+    return torch.cat(parts).double().cpu().numpy()
+
+
+def _assert_nonfinite_parity(got, want, x, ch, tag):
+    """Every output's NaN / +Inf / -Inf class equals the reference's (dft_stage.go:259,531,
+    polyphase_stage.go:288 multiply only an output's real taps)."""
+    for c in range(ch):
+        w = np.asarray(want[c])
+        assert got.shape[0] == len(w), (tag, c)
+        for k, (mg, mw) in enumerate(zip(_nf_sets(got[:, c]), _nf_sets(w))):
+            assert np.array_equal(mg, mw), (tag, c, ("nan", "+inf", "-inf")[k], int((mg & ~mw).sum()), int((mw & ~mg).sum()),
+                                            int((~np.isfinite(x[:, c])).sum()))
+
+
 @pytest.mark.parametrize("case", LOUD, ids=[f"{a}-{b}-{p[7:]}-{c}ch-{'nf' if f else 'loud'}-{k}" for a, b, p, c, f, k, _ in LOUD])
 def test_loud_and_nonfinite_sweep(gar, O, cuda, case):
     """Samples outside the split-f16 range (|x| >= 16 - 2^-8: runs scaled by 40 .. 1e5, single spikes) and,
-    in some cases, Inf / NaN at random places, on float32 compute: non-finite wherever the oracle is,
-    finite values within the error exact-f32 arithmetic makes on the same signal, and any chunking
-    gives the one-shot bits."""
-    import torch
+    in some cases, Inf / NaN at random places: on F32 (split-f16 kernels), F32_EXACT and F64 (the plain
+    MFMA programs, bg_* kernels) every output is NaN / +Inf / -Inf exactly where the reference's is,
+    finite values are within the error the arithmetic makes on the same signal, and any chunking gives
+    the one-shot bits -- NaN positions included."""
     ir, orr, preset, ch, nonfinite, chunk, s0 = case
     rng = np.random.default_rng(s0)
     frames = 12000
@@ -489,46 +522,50 @@ def test_loud_and_nonfinite_sweep(gar, O, cuda, case):
         for v in (np.inf, -np.inf, np.nan)[: int(rng.integers(1, 4))]:
             x[int(rng.integers(frames)), int(rng.integers(ch))] = v
     x = x.astype(np.float32).astype(np.float64)
-
-    def run(dtype, ck):
-        r = gar.New(gar.Config(ir, orr, ch, getattr(gar, preset), ComputeDtype=dtype))
-        xd = torch.from_numpy(np.ascontiguousarray(x)).float().cuda()
-        parts, s = [], 0
-        for n in (chunk_sizes(frames, ck) if ck else [frames]):
-            parts.append(r.process_device(xd[s:s + n]).clone())
-            s += n
-        parts.append(r.flush_device(dtype=torch.float32).clone())
-        torch.cuda.synchronize()
-        return torch.cat(parts).double().cpu().numpy()
-
-    got = run(gar.F32, chunk)
-    ex = run(gar.F32_EXACT, None)
     want = oracle_new(O, ir, orr, x, getattr(O, "P_" + preset[7:].upper()))
+
+    got = _run_stream(gar, ir, orr, ch, preset, gar.F32, x, chunk)
+    ex = _run_stream(gar, ir, orr, ch, preset, gar.F32_EXACT, x, None)
+    _assert_nonfinite_parity(got, want, x, ch, "F32")
+    _assert_nonfinite_parity(ex, want, x, ch, "F32_EXACT")
     for c in range(ch):
         w = np.asarray(want[c])
-        assert got.shape[0] == len(w)
-        nf_w, nf_g = ~np.isfinite(w), ~np.isfinite(got[:, c])
-        # every output the reference makes non-finite is non-finite here; on plans that run on plain
-        # MFMA programs (not the split-f16 kernels: e.g. a long f32 decimator) an Inf / NaN sample
-        # under a zero-padded tap of an output's band also gives NaN (0 * Inf): at most the padding
-        # (< 2 steps of 32 rows) per non-finite input sample of the channel -- DESIGN.md section 5
-        assert not (nf_w & ~nf_g).any(), c
-        n_in = int((~np.isfinite(x[:, c])).sum())
-        assert int((nf_g & ~nf_w).sum()) <= 64 * n_in, (c, int((nf_g & ~nf_w).sum()))
-        fin = ~nf_w & ~nf_g
-        fe = np.isfinite(ex[:, c]) & fin
-        assert rms(got[fin, c], w[fin]) <= max(3.0 * rms(ex[fe, c], w[fe]), F32_RMS_TOL), c
+        fin = np.isfinite(w)
+        assert rms(got[fin, c], w[fin]) <= max(3.0 * rms(ex[fin, c], w[fin]), F32_RMS_TOL), c
     if chunk:
-        one = run(gar.F32, None)
-        if not nonfinite:
-            np.testing.assert_array_equal(got, one)
-        else:
-            # the padded-tap NaNs sit where the MFMA tiles fall, which a call boundary moves (seed 11:
-            # 192k -> 88.2k VeryHigh, 4096-frame calls): same bits wherever both are finite, and the
-            # one-shot run meets the same non-finite contract
-            both = np.isfinite(got) & np.isfinite(one)
-            np.testing.assert_array_equal(got[both], one[both])
-            for c in range(ch):
-                nf_w, nf_o = ~np.isfinite(np.asarray(want[c])), ~np.isfinite(one[:, c])
-                assert not (nf_w & ~nf_o).any(), c
-                assert int((nf_o & ~nf_w).sum()) <= 64 * int((~np.isfinite(x[:, c])).sum()), c
+        np.testing.assert_array_equal(got, _run_stream(gar, ir, orr, ch, preset, gar.F32, x, None))
+    if nonfinite:  # the exact programs: F32_EXACT and F64 chunked == one-shot, F64 within the f64 bar
+        np.testing.assert_array_equal(_run_stream(gar, ir, orr, ch, preset, gar.F32_EXACT, x, chunk or 1111), ex)
+        d1 = _run_stream(gar, ir, orr, ch, preset, gar.F64, x, None)
+        _assert_nonfinite_parity(d1, want, x, ch, "F64")
+        np.testing.assert_array_equal(_run_stream(gar, ir, orr, ch, preset, gar.F64, x, chunk or 4096), d1)
+        for c in range(ch):
+            w = np.asarray(want[c])
+            fin = np.isfinite(w)
+            assert rms(d1[fin, c], w[fin]) <= F64_RMS_TOL * max(1.0, float(np.abs(w[fin]).max(initial=0.0))), c
+
+
+@pytest.mark.parametrize("dtype", ["F64", "F32_EXACT", "F32"])
+def test_nonfinite_cfg5_geometry(gar, O, cuda, dtype):
+    """BASELINE config 5's geometry (8-channel 96k -> 44.1k VeryHigh: integer decimator, then DFT x2 +
+    polyphase, streamed in 4800-frame ProcessInto-sized calls) with +Inf in one channel, -Inf and NaN
+    in two others: the decimator's and the composite's outputs are non-finite exactly where the
+    reference's are (no padded-tap NaNs), and the 4800-frame stream equals the one-shot run bit for bit."""
+    ch, frames = 8, 4800 * 12
+    x = signal(frames, ch, 96000, seed=96)
+    x[20011, 3] = np.inf
+    x[33333, 5] = -np.inf
+    x[4800 * 7 + 5, 0] = np.nan  # just past a call boundary
+    if dtype != "F64":
+        x = x.astype(np.float32).astype(np.float64)
+    want = oracle_new(O, 96000, 44100, x, O.P_VERYHIGH)
+    dt = getattr(gar, dtype)
+    got = _run_stream(gar, 96000, 44100, ch, "QualityVeryHigh", dt, x, 4800)
+    _assert_nonfinite_parity(got, want, x, ch, dtype)
+    np.testing.assert_array_equal(got, _run_stream(gar, 96000, 44100, ch, "QualityVeryHigh", dt, x, None))
+    tol = F64_RMS_TOL if dtype == "F64" else F32_RMS_TOL
+    for c in range(ch):
+        w = np.asarray(want[c])
+        fin = np.isfinite(w)
+        assert (~fin).sum() > 0 or np.isfinite(x[:, c]).all(), c
+        assert rms(got[fin, c], w[fin]) <= tol, (c, rms(got[fin, c], w[fin]))
