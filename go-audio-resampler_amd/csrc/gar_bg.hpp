@@ -69,52 +69,39 @@ __device__ __forceinline__ void outWrite(const OutDesc& o, int64_t idx, int c, T
 __device__ __forceinline__ bool bgFinite(double v) { return __builtin_isfinite(v); }
 __device__ __forceinline__ bool bgFinite(float v) { return __builtin_isfinite(v); }
 
+// The bg kernels' arguments as ONE kernel argument, so the rare non-finite path can read them
+// through the kernarg segment pointer (bgCold) at the point of use: as plain arguments the
+// compiler loads every field that path touches into SGPRs at kernel entry, where they spill
+// (v_writelane / v_readlane in the hot loops; measured r06: cfg5 calls +25 %).
+// (GAR_BG_NF_ATTR: the rare path as out-of-line calls by default; A/B builds __forceinline__)
+#ifndef GAR_BG_NF_ATTR
+#define GAR_BG_NF_ATTR __noinline__
+#endif
+// A struct in the kernarg segment (address space 4) copied out at the point of use.
+template <class T>
+__device__ __forceinline__ T kload(const __attribute__((address_space(4))) T* p) {
+    T v;
+    __builtin_memcpy(&v, (const T*)p, sizeof(T));
+    return v;
+}
+struct BgArgs;
+typedef const __attribute__((address_space(4))) BgArgs* BgArgsP;
+__device__ __forceinline__ BgArgsP bgCold() {
+    uint64_t v = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(v));  // opaque: no field of it is hoisted into the hot path
+    return reinterpret_cast<BgArgsP>(v);
+}
+
 // Output (a, r) of channel c: recomputed and stored when its real window holds a non-finite sample.
 template <class TC>
-__device__ __noinline__ void bgNfFixOne(const BgDev& p, const SrcDesc& src, const OutDesc& od, int64_t a, int r, int c) {
-    const int64_t o = a * p.Pc + r;
-    if (o < od.o_lo || o >= od.o_hi) return;
-    const int* xi = p.xInfo;
-    const int64_t t = a * p.Qc + xi[r];
-    const int len = xi[p.Pc + r];
-    const double* row = p.xRows + static_cast<size_t>(r) * p.xRowMax;
-    double s = 0.0, z = 0.0;
-    for (int k = 0; k < len; ++k) {
-        const double v = static_cast<double>(srcRead<TC>(src, t + k, c));
-        s += row[k] * v;
-        z += v * 0.0;
-    }
-    if (z == z) return;  // the real window is finite: the MFMA value stands
-    if (p.xTwoStage) {   // u = DFT x2 of the window, then the polyphase row (dft_stage.go:259, polyphase_stage.go:288)
-        const int ph = xi[2 * p.Pc + r], par = xi[3 * p.Pc + r], T1 = p.xT1, T2 = p.xT2;
-        const double* pa = p.xPolyA + static_cast<size_t>(ph) * T2;
-        double y = 0.0;
-        for (int k2 = 0; k2 < T2; ++k2) {
-            const int q = par + k2;
-            const double* cq = p.xDftC + static_cast<size_t>(q & 1) * T1;
-            double u = 0.0;
-            for (int k1 = 0; k1 < T1; ++k1) u += cq[k1] * static_cast<double>(srcRead<TC>(src, t + (q >> 1) + k1, c));
-            y += pa[k2] * u;
-        }
-        s = y;
-    }
-    outWrite<TC>(od, o, c, static_cast<TC>(s));
-}
+__device__ GAR_BG_NF_ATTR void bgNfFixOne(BgArgsP ka, int64_t a, int r, int c);
 
 // The outputs (a0 + i, r), i < na, r0 <= r < r1, of channel c whose real window (rows i*Qc + off[r]
 // .. + len[r] relative to input a0*Qc) meets the rows [lo, hi] where non-finite samples were staged;
 // thread tid of nth.
 template <class TC>
-__device__ void bgNfFixRange(const BgDev& p, const SrcDesc& src, const OutDesc& od, int64_t a0, int na, int r0, int r1,
-                             int c, int lo, int hi, int tid, int nth) {
-    const int nr = r1 - r0;
-    for (int idx = tid; idx < na * nr; idx += nth) {
-        const int i = idx / nr, r = r0 + (idx - i * nr);
-        const int w0 = i * p.Qc + p.xInfo[r], w1 = w0 + p.xInfo[p.Pc + r];
-        if (w1 <= lo || w0 > hi) continue;
-        bgNfFixOne<TC>(p, src, od, a0 + i, r, c);
-    }
-}
+__device__ GAR_BG_NF_ATTR void bgNfFixRange(BgArgsP ka, int64_t a0, int na, int r0, int r1, int c, int lo, int hi, int tid,
+                                          int nth);
 
 // ---------------------------------------------------------------------------
 // Banded GEMM.  Geometry (host computed in launchBg):
@@ -133,7 +120,7 @@ __device__ void bgNfFixRange(const BgDev& p, const SrcDesc& src, const OutDesc& 
 #define GAR_BG_DEV 0
 #endif
 constexpr bool kBgDev = GAR_BG_DEV;
-constexpr size_t kBgStaticLds = 1152;  // bg_kernel's static LDS (nfFlag / nfLo / nfHi: 1032 B), rounded up
+constexpr size_t kBgStaticLds = 64;  // bg_kernel's static LDS (nfFlag), rounded up
 constexpr int kBgProfWords = 64;
 
 struct BgGrid {
@@ -182,6 +169,61 @@ struct BgStamps {
         }
     }
 };
+
+struct BgArgs {
+    BgDev p;
+    SrcDesc src;
+    OutDesc od;
+    BgGrid g;
+};
+
+template <class TC>
+__device__ GAR_BG_NF_ATTR void bgNfFixOne(BgArgsP ka, int64_t a, int r, int c) {
+    const BgDev p = kload(&ka->p);
+    const SrcDesc src = kload(&ka->src);
+    const OutDesc od = kload(&ka->od);
+    const int64_t o = a * p.Pc + r;
+    if (o < od.o_lo || o >= od.o_hi) return;
+    const int* xi = p.xInfo;
+    const int64_t t = a * p.Qc + xi[r];
+    const int len = xi[p.Pc + r];
+    const double* row = p.xRows + static_cast<size_t>(r) * p.xRowMax;
+    double s = 0.0, z = 0.0;
+    for (int k = 0; k < len; ++k) {
+        const double v = static_cast<double>(srcRead<TC>(src, t + k, c));
+        s += row[k] * v;
+        z += v * 0.0;
+    }
+    if (z == z) return;  // the real window is finite: the MFMA value stands
+    if (p.xTwoStage) {   // u = DFT x2 of the window, then the polyphase row (dft_stage.go:259, polyphase_stage.go:288)
+        const int ph = xi[2 * p.Pc + r], par = xi[3 * p.Pc + r], T1 = p.xT1, T2 = p.xT2;
+        const double* pa = p.xPolyA + static_cast<size_t>(ph) * T2;
+        double y = 0.0;
+        for (int k2 = 0; k2 < T2; ++k2) {
+            const int q = par + k2;
+            const double* cq = p.xDftC + static_cast<size_t>(q & 1) * T1;
+            double u = 0.0;
+            for (int k1 = 0; k1 < T1; ++k1) u += cq[k1] * static_cast<double>(srcRead<TC>(src, t + (q >> 1) + k1, c));
+            y += pa[k2] * u;
+        }
+        s = y;
+    }
+    outWrite<TC>(od, o, c, static_cast<TC>(s));
+}
+
+template <class TC>
+__device__ GAR_BG_NF_ATTR void bgNfFixRange(BgArgsP ka, int64_t a0, int na, int r0, int r1, int c, int lo, int hi, int tid,
+                                          int nth) {
+    const int Qc = ka->p.Qc, Pc = ka->p.Pc;
+    const int* xi = ka->p.xInfo;
+    const int nr = r1 - r0;
+    for (int idx = tid; idx < na * nr; idx += nth) {
+        const int i = idx / nr, r = r0 + (idx - i * nr);
+        const int w0 = i * Qc + xi[r], w1 = w0 + xi[Pc + r];
+        if (w1 <= lo || w0 > hi) continue;
+        bgNfFixOne<TC>(ka, a0 + i, r, c);
+    }
+}
 
 // f32 epilogue of one 16x16 accumulator: lane holds rows r0..r0+3 (r0 =
 // rb*16 + 4*(lane>>4)) of column (chunk, c).  vst 1: the four rows are
@@ -431,42 +473,49 @@ __device__ __forceinline__ void segStore(const ProgU& pu, int j, const typename 
 // (global-B: a non-finite sample is read as 0 and flagged in nf; LDS tiles were cleaned by bgNfScan)
 template <class TC, bool GB>
 __device__ __forceinline__ TC fetchB(const TC* bp, const ProgU& pu, int s, const SrcDesc& src, int64_t tb, int c,
-                                     bool colOk, bool same, const void* dummy, bool& nf) {
+                                     bool colOk, bool same, const void* dummy, int& nf) {
     if constexpr (GB) {
         const TC v = colOk ? srcRead<TC>(src, tb + selK(pu, s) + 4 * s, c) : TC(0);
         const bool ok = bgFinite(v);
-        nf |= !ok;
+        nf |= ok ? 0 : 1;
         return ok ? v : TC(0);
     } else {
         return bp[selU(pu, s) + 64 * s];
     }
 }
 
-// Non-finite samples of one LDS sub-tile: the pieces this wave staged (j = wt mod nwt; lane l of a
-// piece wrote dword l) are checked once they have landed; a non-finite element is set to 0 and its
-// (column, row) recorded in this block's parity slot (nfLo / nfHi per column, nfFlag).
+// Non-finite samples of one LDS sub-tile, before the block's barrier: the pieces this wave staged
+// (j = wt mod nwt; lane l of a piece wrote dword l) are read back once they have landed, kB reads in
+// flight (r06: a read -> compare -> branch chain per piece cost the f64 one-shot launches 13 %, this
+// pass 7 %); a non-finite element is set to 0 and the wave flags the block (nf), which bg_kernel then
+// records for bg_nf_kernel.
 template <class TC>
-__device__ __forceinline__ void bgNfScan(TC* sub, const BgGrid& g, int cg, int wt, int lane, int par, int* nfFlag,
-                                         int (*nfLo)[64], int (*nfHi)[64]) {
+__device__ __forceinline__ void bgNfScan(TC* sub, const BgGrid& g, int wt, int lane, int& nf) {
     constexpr int rowsPerPiece = sizeof(TC) == 8 ? 2 : 4;
-    const int np = tilePieces<TC>(g);
+    constexpr int kB = 8;
+    const int np = tilePieces<TC>(g), nwt = g.nwt;
     const int e = sizeof(TC) == 8 ? (lane >> 1) : lane;  // element (row e >> 4, column e & 15) of the piece
     __builtin_amdgcn_s_waitcnt(0);  // this wave's pieces landed (LDS-DMA: vmcnt; gathered stores: lgkmcnt)
-    bool any = false;
-#pragma unroll 4
-    for (int j = wt; j < np; j += g.nwt) {
-        TC* q = sub + static_cast<size_t>(j) * rowsPerPiece * 16 + e;
-        const TC v = *q;
-        if (__builtin_expect(!bgFinite(v), 0)) {
-            *q = TC(0);
-            const int col = cg * 16 + (e & 15), row = j * rowsPerPiece + (e >> 4);
-            atomicMin(&nfLo[par][col], row);
-            atomicMax(&nfHi[par][col], row);
-            any = true;
+    bool bad = false;
+    for (int j0 = wt; j0 < np; j0 += kB * nwt) {
+        TC v[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int j = j0 + u * nwt;
+            v[u] = j < np ? sub[static_cast<size_t>(j) * rowsPerPiece * 16 + e] : TC(0);
         }
+#pragma unroll
+        for (int u = 0; u < kB; ++u) bad |= !bgFinite(v[u]);
     }
-    if (any) nfFlag[par] = 1;
+    if (__builtin_expect(__any(bad), 0)) {  // rare: clean this wave's pieces
+        for (int j = wt; j < np; j += nwt) {
+            TC* q = sub + static_cast<size_t>(j) * rowsPerPiece * 16 + e;
+            if (!bgFinite(*q)) *q = TC(0);
+        }
+        nf = 1;
+    }
 }
+
 
 // In-loop segment boundary: bank the running sum (stores happen after the loop).
 // (e1, e2 are segment starts, always inside the program, or 1<<20 if unused)
@@ -477,11 +526,75 @@ __device__ __forceinline__ void bgNfScan(TC* sub, const BgGrid& g, int cg, int w
         r1 = acc0 + acc1; acc0 = V{0, 0, 0, 0}; acc1 = acc0; \
     }
 
+// bg_kernel's non-finite fix list (BgDev::nfList, zeroed between launches by bg_nf_kernel):
+// [0] entries, [1] overflow, then kBgNfEntry ints per entry (block, lo[64], hi[64]), then a done
+// counter.  bg_kernel only records (a block that staged a non-finite sample adds its column ranges;
+// the fixup code would cost the persistent loop registers), bg_nf_kernel -- launched after every
+// bg_kernel launch, it returns at once when the list is empty -- recomputes the outputs.
+constexpr int kBgNfEntry = 1 + 2 * 64;  // block (+ room for per-column row ranges, unused: whole blocks are checked)
+constexpr int kBgNfCap = 256;
+constexpr int kBgNfInts = 2 + kBgNfCap * kBgNfEntry + 1;
+static_assert(kBgNfListBytes == 4 * kBgNfInts, "the host allocates kBgNfListBytes for the list");
+
+// bg_kernel / bg_nf_kernel: the fixup of block b (every column with a recorded row range; global-B:
+// every output of the block).
+template <class TC, bool GLOBAL_B>
+__device__ GAR_BG_NF_ATTR void bgNfFixBlock(BgArgsP ka, int b, const int* nfLo, const int* nfHi) {
+    const int ncg = ka->g.ncg, ncols = ka->g.ncols, C = ka->g.C, G = ka->g.G, Pc = ka->g.Pc;
+    const int64_t a_lo = ka->g.a_lo;
+    for (int cl = 0; cl < 16 * ncg; ++cl) {
+        const int colx = b * 16 * ncg + cl;
+        if (colx >= ncols) break;
+        const int lo = GLOBAL_B ? 0 : nfLo[cl], hi = GLOBAL_B ? (1 << 30) : nfHi[cl];
+        if (hi < 0) continue;
+        const int chx = colx / C;
+        bgNfFixRange<TC>(ka, a_lo + static_cast<int64_t>(chx) * G, G, 0, Pc, colx - chx * C, lo, hi, threadIdx.x, blockDim.x);
+    }
+}
+
+// Wave 0 of bg_kernel: block b into the fix list (bg_nf_kernel checks every output of it).
+__device__ __forceinline__ void bgNfRecord(int* list, int b, int lane) {
+    if (lane == 0) {
+        const int e = atomicAdd(list, 1);
+        if (e < kBgNfCap) list[2 + e * kBgNfEntry] = b;
+        else list[1] = 1;  // overflow: bg_nf_kernel checks every block
+    }
+}
+
+// After every bg_kernel launch: the outputs of the recorded blocks whose real window holds a
+// non-finite sample get the reference's values; the list is emptied for the next launch (by the
+// last workgroup out).  An empty list returns at once.
+template <class TC>
+__global__ __launch_bounds__(256) void bg_nf_kernel(BgArgs ka) {
+    int* L = ka.p.nfList;
+    const int n = *reinterpret_cast<volatile int*>(L), ovf = *reinterpret_cast<volatile int*>(L + 1);
+    if (n == 0 && ovf == 0) return;
+    const BgArgsP kp = bgCold();
+    if (ovf) {
+        for (int b = blockIdx.x; b < ka.g.nblocks; b += gridDim.x) bgNfFixBlock<TC, true>(kp, b, nullptr, nullptr);
+    } else {
+        for (int e = blockIdx.x; e < min(n, kBgNfCap); e += gridDim.x) bgNfFixBlock<TC, true>(kp, L[2 + e * kBgNfEntry], nullptr, nullptr);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(L + kBgNfInts - 1, 1) == static_cast<int>(gridDim.x) - 1) {
+            L[0] = 0;
+            L[1] = 0;
+            L[kBgNfInts - 1] = 0;
+            __threadfence();
+        }
+    }
+}
+
 // Prefetch-free persistent kernel: the next block's tile arrives by LDS-DMA
 // (issued 1/G per macro-period iteration) while the current block computes.
 template <class TC, int NS, bool GLOBAL_B, bool SINGLE>
-__global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(BgDev p, SrcDesc src, OutDesc od,
-                                                                               BgGrid g) {
+__global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(BgArgs ka) {
+    const BgDev& p = ka.p;
+    const SrcDesc& src = ka.src;
+    const OutDesc& od = ka.od;
+    const BgGrid& g = ka.g;
     typedef typename Acc<TC>::V V;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int subElems = g.Ws * 16;                           // one column group's sub-tile
@@ -499,12 +612,14 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     const TC* Aimg = static_cast<const TC*>(p.A);
     const bool same = srcSameType<TC>(src);
 
-    // non-finite samples staged per block parity (bgNfScan): flag + row range per column
-    __shared__ int nfFlag[2], nfLo[2][64], nfHi[2][64];
-    for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) { (&nfLo[0][0])[i] = 0x7fffffff; (&nfHi[0][0])[i] = -1; }
-    if (threadIdx.x < 2) nfFlag[threadIdx.x] = 0;
+    // a wave that staged (or, global-B, read) a non-finite sample of block b (parity it & 1) writes b + 1 here; wave 0
+    // records the block for bg_nf_kernel after the next barrier (block indices are unique per
+    // workgroup, so the slot needs no reset)
+    __shared__ int nfFlag[2];
+    if (threadIdx.x < 2) nfFlag[threadIdx.x] = -1;
     __syncthreads();
-    bool nfl = false;  // global-B: this lane read a non-finite sample in the current block
+    int nfl = 0;  // this wave staged / read a non-finite sample of the current block
+    int bPrev = -1, parPrev = 0;
 
     TC A[NS];
     if (SINGLE && wt < g.nprog) {
@@ -517,10 +632,9 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
     int q = 0;  // macro-period iteration counter (partial-slot parity)
     for (int it = 0; b < g.nblocks; b += gridDim.x, ++it) {
         TC* tile = tiles + static_cast<size_t>(it & 1) * tileElems + cg * subElems;
-        if (!GLOBAL_B) bgNfScan<TC>(tile, g, cg, wt, lane, it & 1, nfFlag, nfLo, nfHi);
+        if (!GLOBAL_B) bgNfScan<TC>(tile, g, wt, lane, nfl);
         __syncthreads();  // this tile's DMA landed (vmcnt) + the other buffer is free
-        // read right after the barrier: the slot of this parity is written again only after the next one
-        const bool nfB = !GLOBAL_B && nfFlag[it & 1] != 0;
+        if (wave == 0 && bPrev >= 0 && nfFlag[(it + 1) & 1] == bPrev + 1) bgNfRecord(p.nfList, bPrev, lane);
         const int bn = b + gridDim.x;
         const bool pre = !GLOBAL_B && bn < g.nblocks && !(g.dbg & 1);
         TC* ntile = tiles + static_cast<size_t>((it + 1) & 1) * tileElems + cg * subElems;
@@ -615,26 +729,14 @@ __global__ __launch_bounds__(bgMaxThreads(sizeof(TC) == 8, NS)) void bg_kernel(B
                 if (!g.parity) __syncthreads();
             }
         }
-        // outputs of this block whose real window holds a non-finite sample: the reference's values
-        bool fix = nfB;
-        if constexpr (GLOBAL_B) { fix = __syncthreads_or(nfl); nfl = false; }
-        if (fix) {
-            __syncthreads();  // every output of the block stored (vmcnt(0) + barrier) before it is overwritten
-            for (int cl = 0; cl < 16 * g.ncg; ++cl) {
-                const int colx = b * 16 * g.ncg + cl;
-                if (colx >= g.ncols) break;
-                const int lo = GLOBAL_B ? 0 : nfLo[it & 1][cl], hi = GLOBAL_B ? (1 << 30) : nfHi[it & 1][cl];
-                if (hi < 0) continue;
-                const int chx = colx / g.C;
-                bgNfFixRange<TC>(p, src, od, g.a_lo + static_cast<int64_t>(chx) * g.G, g.G, 0, g.Pc, colx - chx * g.C, lo, hi,
-                                 threadIdx.x, blockDim.x);
-            }
-            __syncthreads();  // this parity's ranges read by every wave
-            if (!GLOBAL_B) {
-                for (int i = threadIdx.x; i < 64; i += blockDim.x) { nfLo[it & 1][i] = 0x7fffffff; nfHi[it & 1][i] = -1; }
-                if (threadIdx.x == 0) nfFlag[it & 1] = 0;
-            }
-        }
+        if (__builtin_expect(__any(nfl), 0) && lane == 0) nfFlag[it & 1] = b + 1;
+        nfl = 0;
+        bPrev = b;
+        parPrev = it & 1;
+    }
+    if (bPrev >= 0) {  // the workgroup's last block
+        __syncthreads();
+        if (wave == 0 && nfFlag[parPrev] == bPrev + 1) bgNfRecord(p.nfList, bPrev, lane);
     }
     if (g.hn > 0) {  // history keep for the next call (launchGather's job, folded into this launch)
         const int64_t total = g.hn * g.C;
@@ -673,41 +775,75 @@ __device__ __forceinline__ void bgRbHistKeep(const SrcDesc& src, const BgGrid& g
     bgRbHistKeepW<TC>(src, g, blockIdx.x, gridDim.x);
 }
 
-// One (column block, row block) item v of a bg_rb_kernel launch.  keep: this workgroup's share
-// (workgroup wg of nwg) of the history keep rides on this item.
-// Non-finite bookkeeping of the small launches, per wave (each wave writes only its own entries,
-// other waves read them between two barriers, the owner resets them after the item): bg_rb_kernel
-// keeps a row range per column of the item (rows relative to the column's a * Qc), bg_rt_kernel one
-// range (rows of the staged window).
+// Non-finite samples on the small launches (bg_rb_kernel, bg_rt_kernel): the hot path is the
+// finite one -- the item runs as always, and only its final values are checked (a non-finite sample
+// under any tap, padded or real, makes the output non-finite).  An item whose outputs hold a
+// non-finite value is redone out of line: its samples staged with every non-finite one as 0 (the
+// value the band gives with that sample zero, the same bits in every kernel and chunking), then the
+// outputs whose REAL window holds a non-finite sample recomputed in the reference's order
+// (bgNfFixOne).  Per-wave row ranges: each wave writes only its own entries.
 struct BgNfRb {
-    int lo[kBgRbMaxWaves][16], hi[kBgRbMaxWaves][16], any[kBgRbMaxWaves];
+    int lo[kBgRbMaxWaves][16], hi[kBgRbMaxWaves][16];
 };
-__device__ __forceinline__ void bgNfRbInit(BgNfRb& nf, int wt, int lane) {
-    if (lane < 16) { nf.lo[wt][lane] = 0x7fffffff; nf.hi[wt][lane] = -1; }
-    if (lane == 0) nf.any[wt] = 0;
+
+template <class V>
+__device__ __forceinline__ bool bgAccFinite(const V& v) {
+    return bgFinite(v[0]) && bgFinite(v[1]) && bgFinite(v[2]) && bgFinite(v[3]);
+}
+
+// One program of a bg_rb_kernel item (wave wt < np): A and B loaded, B's non-finite elements set to
+// 0 and their rows (k0 + 4 s + lane / 16, relative to the column's a * Qc) recorded, the MFMA chain
+// of bgRbItem.  Out of line: the redo of an item whose outputs were non-finite.
+template <class TC, int NS>
+__device__ GAR_BG_NF_ATTR typename Acc<TC>::V bgRbProgClean(BgArgsP ka, int pr, int64_t a, int c, bool colOk, int wt,
+                                                            int lane, BgNfRb* nf) {
+    typedef typename Acc<TC>::V V;
+    const SrcDesc src = kload(&ka->src);
+    const TC* Aimg = static_cast<const TC*>(ka->p.A);
+    const int k0 = ka->g.rbK0[pr], Qc = ka->g.Qc;
+    if (lane < 16) { nf->lo[wt][lane] = 0x7fffffff; nf->hi[wt][lane] = -1; }
+    V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+    for (int s = 0; s < NS; ++s) {
+        const int rr = k0 + 4 * s + (lane >> 4);
+        TC bv = colOk ? srcRead<TC>(src, a * Qc + rr, c) : TC(0);
+        if (!bgFinite(bv)) {
+            bv = TC(0);
+            atomicMin(&nf->lo[wt][lane & 15], rr);
+            atomicMax(&nf->hi[wt][lane & 15], rr);
+        }
+        const TC av = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+        if (s & 1) acc1 = Acc<TC>::mfma(av, bv, acc1);
+        else acc0 = Acc<TC>::mfma(av, bv, acc0);
+    }
+    return acc0 + acc1;
 }
 
 // Item (column block b, row block rb) of bg_rb_kernel: its outputs whose real window meets a
 // recorded row range (waves < np) -- thread tid of nth.
 template <class TC>
-__device__ void bgRbFix(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int b, int rb, int np,
-                        const BgNfRb& nf, int tid, int nth) {
+__device__ GAR_BG_NF_ATTR void bgRbFix(BgArgsP ka, int b, int rb, int np, const BgNfRb* nf, int tid, int nth) {
+    const int Pc = ka->g.Pc, ncols = ka->g.ncols, C = ka->g.C;
+    const int64_t a_lo = ka->g.a_lo;
+    const int* xi = ka->p.xInfo;
     for (int idx = tid; idx < 256; idx += nth) {
         const int n = idx & 15, r = rb * 16 + (idx >> 4);
         const int col = b * 16 + n;
-        if (r >= g.Pc || col >= g.ncols) continue;
+        if (r >= Pc || col >= ncols) continue;
         int lo = 0x7fffffff, hi = -1;
-        for (int w = 0; w < np; ++w) { lo = min(lo, nf.lo[w][n]); hi = max(hi, nf.hi[w][n]); }
+        for (int w = 0; w < np; ++w) { lo = min(lo, nf->lo[w][n]); hi = max(hi, nf->hi[w][n]); }
         if (hi < 0) continue;
-        const int w0 = p.xInfo[r], w1 = w0 + p.xInfo[p.Pc + r];
+        const int w0 = xi[r], w1 = w0 + xi[Pc + r];
         if (w1 <= lo || w0 > hi) continue;
-        bgNfFixOne<TC>(p, src, od, g.a_lo + col / g.C, r, col % g.C);
+        bgNfFixOne<TC>(ka, a_lo + col / C, r, col % C);
     }
 }
 
+// One (column block, row block) item v of a bg_rb_kernel launch.  keep: this workgroup's share
+// (workgroup wg of nwg) of the history keep rides on this item.
 template <class TC, int NS>
 __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
-                                         typename Acc<TC>::V (*slots)[64], bool keep, int wg, int nwg, BgNfRb& nf) {
+                                         typename Acc<TC>::V (*slots)[64], bool keep, int wg, int nwg, BgNfRb& nf,
+                                         int* nfItem) {
     typedef typename Acc<TC>::V V;
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
@@ -769,53 +905,41 @@ __device__ __forceinline__ void bgRbItem(const BgDev& p, const SrcDesc& src, con
             else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
         }
         r = acc0 + acc1;
-        // non-finite B (checked beside the MFMA chain; rare): stage them as 0, record their rows, rerun
-        bool bad = false;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) bad |= !bgFinite(B[s]);
-        if (__builtin_expect(__any(bad), 0)) {
-#pragma unroll
-            for (int s = 0; s < NS; ++s)
-                if (!bgFinite(B[s])) {
-                    B[s] = TC(0);
-                    atomicMin(&nf.lo[wt][lane & 15], k0 + 4 * s + (lane >> 4));
-                    atomicMax(&nf.hi[wt][lane & 15], k0 + 4 * s + (lane >> 4));
-                }
-            if (lane == 0) nf.any[wt] = 1;
-            acc0 = V{0, 0, 0, 0};
-            acc1 = acc0;
-#pragma unroll
-            for (int s = 0; s < NS; ++s) {
-                if (s & 1) acc1 = Acc<TC>::mfma(A[s], B[s], acc1);
-                else acc0 = Acc<TC>::mfma(A[s], B[s], acc0);
-            }
-            r = acc0 + acc1;
-        }
         if (np > 1) slots[wt][lane] = r;
         if (kBgDev && stm.on) { __builtin_amdgcn_s_waitcnt(0); stm.mark(); }  // MFMA chain done
     }
     if (np > 1) {
         __syncthreads();
         stm.mark();  // reduction barrier
-        bool fix = false;  // a wave of this item staged a non-finite sample (uniform: read between barriers)
-        for (int w = 0; w < np; ++w) fix |= nf.any[w] != 0;
         if (wt == 0) {
             V sum = slots[0][lane];
             for (int k = 1; k < np; ++k) sum += slots[k][lane];
             if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            if (__builtin_expect(__any(!bgAccFinite(sum)), 0) && lane == 0) *nfItem = v + 1;
         }
         __syncthreads();  // slots free for the next (column block, row block); wave 0's stores done
-        if (fix) {
-            bgRbFix<TC>(p, src, od, g, b, rb, np, nf, threadIdx.x, blockDim.x);
-            __syncthreads();  // every wave read the ranges
-            if (wt < np && nf.any[wt]) bgNfRbInit(nf, wt, lane);
+        if (__builtin_expect(*nfItem == v + 1, 0)) {  // uniform: redo the item with the non-finite samples as 0
+            const BgArgsP ka = bgCold();
+            if (wt < np) slots[wt][lane] = bgRbProgClean<TC, NS>(ka, ps + wt, a, c, colOk, wt, lane, &nf);
+            __syncthreads();
+            if (wt == 0) {
+                V sum = slots[0][lane];
+                for (int k = 1; k < np; ++k) sum += slots[k][lane];
+                storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            }
+            __syncthreads();  // the clean outputs stored, every wave's ranges recorded
+            bgRbFix<TC>(ka, b, rb, np, &nf, threadIdx.x, blockDim.x);
+            __syncthreads();  // slots and ranges free
         }
     } else if (wt == 0) {
         if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
-        if (nf.any[0]) {  // the item's only wave: fix its outputs itself, after its own stores
-            __builtin_amdgcn_s_waitcnt(0);
-            bgRbFix<TC>(p, src, od, g, b, rb, 1, nf, lane, 64);
-            bgNfRbInit(nf, 0, lane);
+        if (__builtin_expect(__any(!bgAccFinite(r)), 0)) {  // the item's only wave redoes it alone
+            const BgArgsP ka = bgCold();
+            const V rc = bgRbProgClean<TC, NS>(ka, ps, a, c, colOk, 0, lane, &nf);
+            __builtin_amdgcn_s_waitcnt(0);  // the first stores landed before the clean ones
+            storeAcc<TC>(od, g, a, rb, c, colOk, rc, lane);
+            __builtin_amdgcn_s_waitcnt(0);  // its stores landed before the fixup overwrites some
+            bgRbFix<TC>(ka, b, rb, 1, &nf, lane, 64);
         }
     }
     stm.done(g, 32);
@@ -836,17 +960,22 @@ __device__ __forceinline__ bool bgXcdItem(int64_t bb, int M, int ngroups, int& g
 }
 
 template <class TC, int NS>
-__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rb_kernel(BgArgs ka) {
+    const BgDev& p = ka.p;
+    const SrcDesc& src = ka.src;
+    const OutDesc& od = ka.od;
+    const BgGrid& g = ka.g;
     typedef typename Acc<TC>::V V;
     __shared__ V slots[kBgRbMaxWaves][64];
     __shared__ BgNfRb nf;
-    bgNfRbInit(nf, threadIdx.x >> 6, threadIdx.x & 63);  // each wave its own entries (no barrier needed)
+    __shared__ int nfItem;  // item + 1 whose outputs hold a non-finite value (written by wave 0 only)
+    if (threadIdx.x == 0) nfItem = -1;
     const int64_t total = bgXcdSlots(g.nblocks, p.nrb);
     bool kept = false;
     for (int64_t bb = blockIdx.x; bb < total; bb += gridDim.x) {  // uniform per workgroup
         int b, rb;
         if (!bgXcdItem(bb, p.nrb, g.nblocks, b, rb)) continue;
-        bgRbItem<TC, NS>(p, src, od, g, b * p.nrb + rb, slots, !kept, blockIdx.x, gridDim.x, nf);
+        bgRbItem<TC, NS>(p, src, od, g, b * p.nrb + rb, slots, !kept, blockIdx.x, gridDim.x, nf, &nfItem);
         kept = true;
     }
     if (!kept) bgRbHistKeep<TC>(src, g);  // a workgroup without an item
@@ -867,10 +996,75 @@ inline size_t bgRtLds(int Qc, int Kread, int nprog, size_t esz) {
     return (win + 15) / 16 * 16 + static_cast<size_t>(nprog) * 64 * 4 * esz;
 }
 
+// Redo of a bg_rt_kernel item whose outputs hold a non-finite value (all waves; the window is still
+// in LDS): its non-finite samples set to 0 and their rows recorded (nf[0] lo, nf[1] hi), the programs
+// rerun from the clean window, the sums stored, then the outputs whose real window holds a non-finite
+// sample recomputed (bgNfFixRange).
+template <class TC, int NS>
+__device__ GAR_BG_NF_ATTR void bgRtRedo(BgArgsP ka, int v, unsigned char* smem, int* nf) {
+    typedef typename Acc<TC>::V V;
+    const int lane = threadIdx.x & 63, wt = threadIdx.x >> 6;
+    const int Qc = ka->g.Qc, pad = kRtPad(Qc), nrb = ka->p.nrb, Pc = ka->g.Pc, nchunk = ka->g.nchunk;
+    const int nrow = 15 * Qc + ka->g.Wl;
+    const int nphys = nrow + pad * (nrow / Qc + 1);
+    TC* win = reinterpret_cast<TC*>(smem);
+    V* slots = reinterpret_cast<V*>(smem + (static_cast<size_t>(nphys) * sizeof(TC) + 15) / 16 * 16);
+    const int nkb = (nchunk + 15) / 16;
+    const int rb = v % nrb, cb = v / nrb;
+    const int c = cb / nkb, kb = cb - c * nkb;
+    const int ps = ka->g.rbStart[rb], np = ka->g.rbStart[rb + 1] - ps;
+    if (threadIdx.x == 0) { nf[0] = 0x7fffffff; nf[1] = -1; }
+    __syncthreads();
+    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+        TC* e = win + r + pad * (r / Qc);
+        if (!bgFinite(*e)) { *e = TC(0); atomicMin(nf, r); atomicMax(nf + 1, r); }
+    }
+    __syncthreads();  // clean window, ranges final
+    const int n = lane & 15, kq = lane >> 4;
+    const int64_t a = ka->g.a_lo + 16 * static_cast<int64_t>(kb) + n;
+    const bool colOk = 16 * kb + n < nchunk;
+    const OutDesc od = kload(&ka->od);
+    BgGrid g{};  // the fields storeAcc reads
+    g.Pc = Pc;
+    g.vst = ka->g.vst;
+    V r = {0, 0, 0, 0};
+    if (wt < np) {
+        const int pr = ps + wt, k0 = ka->g.rbK0[pr];
+        const TC* Aimg = static_cast<const TC*>(ka->p.A);
+        const int x0 = k0 + kq;
+        int q = x0 / Qc, rem = x0 - q * Qc;
+        const int nb = n * (Qc + pad);
+        V acc0 = {0, 0, 0, 0}, acc1 = acc0;
+        for (int s = 0; s < NS; ++s) {
+            const TC bv = win[nb + q * (Qc + pad) + rem];
+            rem += 4;
+            while (rem >= Qc) { rem -= Qc; ++q; }
+            const TC av = Aimg[(static_cast<size_t>(pr) * NS + s) * 64 + lane];
+            if (s & 1) acc1 = Acc<TC>::mfma(av, bv, acc1);
+            else acc0 = Acc<TC>::mfma(av, bv, acc0);
+        }
+        r = acc0 + acc1;
+        if (np > 1) slots[wt * 64 + lane] = r;
+    }
+    __syncthreads();
+    if (wt == 0) {
+        V sum = r;
+        if (np > 1) {
+            sum = slots[lane];
+            for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
+        }
+        storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+    }
+    __syncthreads();  // the clean outputs stored
+    bgNfFixRange<TC>(ka, ka->g.a_lo + 16 * static_cast<int64_t>(kb), 16, rb * 16, min(rb * 16 + 16, Pc), c, nf[0], nf[1],
+                     threadIdx.x, blockDim.x);
+    __syncthreads();  // window, slots and ranges free
+}
+
 // One (row block, channel, chunk block) item v of a bg_rt_kernel launch (smem: the window + slots).
 template <class TC, int NS>
 __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, const OutDesc& od, const BgGrid& g, int v,
-                                         unsigned char* smem, bool keep, int wg, int nwg, int* nfLo, int* nfHi) {
+                                         unsigned char* smem, bool keep, int wg, int nwg, int* nfItem, int* nf) {
     typedef typename Acc<TC>::V V;
     const int lane = threadIdx.x & 63;
     const int wt = threadIdx.x >> 6;
@@ -907,10 +1101,6 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
 #pragma unroll
         for (int u = 0; u < kRtB; ++u) {
             const int r = r0 + u * blockDim.x;
-            if (__builtin_expect(!bgFinite(vv[u]), 0)) {  // staged as 0, its row recorded (bgNfFixOne)
-                vv[u] = TC(0);
-                if (r < nrow) { atomicMin(&nfLo[wt], r); atomicMax(&nfHi[wt], r); }
-            }
             if (r < nrow) win[r + pad * (r / Qc)] = vv[u];
         }
     }
@@ -918,8 +1108,6 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
     stm.mark();  // A issued, window staged by this wave
     __syncthreads();  // window staged
     stm.mark();
-    int nlo = 0x7fffffff, nhi = -1;  // rows of the window where non-finite samples were staged (uniform)
-    for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) { nlo = min(nlo, nfLo[w]); nhi = max(nhi, nfHi[w]); }
     const int n = lane & 15, kq = lane >> 4;
     const int64_t a = g.a_lo + 16 * static_cast<int64_t>(kb) + n;
     const bool colOk = 16 * kb + n < g.nchunk;
@@ -955,25 +1143,27 @@ __device__ __forceinline__ void bgRtItem(const BgDev& p, const SrcDesc& src, con
             V sum = slots[lane];
             for (int k = 1; k < np; ++k) sum += slots[k * 64 + lane];
             if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, sum, lane);
+            if (__builtin_expect(__any(!bgAccFinite(sum)), 0) && lane == 0) *nfItem = v + 1;
         }
-    } else if (wt == 0 && !(g.dbg & 2)) {
-        storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
-    }
-    if (nhi >= 0) {  // outputs whose real window holds a non-finite sample: the reference's values
-        __syncthreads();  // the item's outputs stored
-        bgNfFixRange<TC>(p, src, od, g.a_lo + 16 * static_cast<int64_t>(kb), 16, rb * 16, min(rb * 16 + 16, g.Pc), c, nlo, nhi,
-                         threadIdx.x, blockDim.x);
+    } else if (wt == 0) {
+        if (!(g.dbg & 2)) storeAcc<TC>(od, g, a, rb, c, colOk, r, lane);
+        if (__builtin_expect(__any(!bgAccFinite(r)), 0) && lane == 0) *nfItem = v + 1;
     }
     __syncthreads();  // window and slots free for the next (row block, channel, chunk block)
-    if (nhi >= 0 && lane == 0) { nfLo[wt] = 0x7fffffff; nfHi[wt] = -1; }  // every wave read them before the barrier
+    if (__builtin_expect(*nfItem == v + 1, 0)) bgRtRedo<TC, NS>(bgCold(), v, smem, nf);  // uniform
     stm.done(g, 0);
 }
 
 template <class TC, int NS>
-__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcDesc src, OutDesc od, BgGrid g) {
+__global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgArgs ka) {
+    const BgDev& p = ka.p;
+    const SrcDesc& src = ka.src;
+    const OutDesc& od = ka.od;
+    const BgGrid& g = ka.g;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int nfLo[kBgRbMaxWaves], nfHi[kBgRbMaxWaves];  // per wave: rows of non-finite samples staged
-    if ((threadIdx.x & 63) == 0) { nfLo[threadIdx.x >> 6] = 0x7fffffff; nfHi[threadIdx.x >> 6] = -1; }
+    __shared__ int nfItem;  // item + 1 whose outputs hold a non-finite value (written by wave 0 only)
+    __shared__ int nf[2];   // its rows of non-finite samples (bgRtRedo)
+    if (threadIdx.x == 0) nfItem = -1;
     const int nkb = (g.nchunk + 15) / 16;
     const int M = p.nrb * g.C;  // items of one time block: row blocks x channels
     const int64_t total = bgXcdSlots(nkb, M);
@@ -982,7 +1172,7 @@ __global__ __launch_bounds__(64 * kBgRbMaxWaves) void bg_rt_kernel(BgDev p, SrcD
         int kb, m;
         if (!bgXcdItem(bb, M, nkb, kb, m)) continue;
         const int rb = m % p.nrb, c = m / p.nrb;
-        bgRtItem<TC, NS>(p, src, od, g, rb + p.nrb * (c * nkb + kb), smem, !kept, blockIdx.x, gridDim.x, nfLo, nfHi);
+        bgRtItem<TC, NS>(p, src, od, g, rb + p.nrb * (c * nkb + kb), smem, !kept, blockIdx.x, gridDim.x, &nfItem, nf);
         kept = true;
     }
     // every thread of a workgroup with an item copied its share in its first item (no
@@ -998,14 +1188,15 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
     setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, true>));
     setMaxLdsOnce(reinterpret_cast<const void*>(&bg_kernel<TC, NS, true, false>));
     const dim3 gd(static_cast<unsigned>(blocks)), bd(threads);
+    const BgArgs ka{p, src, od, g};
     if (g.rbMode) {
         if constexpr (sizeof(TC) == 8 && NS <= kBgRbMaxSteps) {
             if (threads > 64 * kBgRbMaxWaves) return hipErrorInvalidConfiguration;
             if (g.rbMode == 2) {  // time-major, LDS-staged windows
                 if (const size_t lim_ = setMaxLdsOnce(reinterpret_cast<const void*>(&bg_rt_kernel<TC, NS>)); lim_ < lds) return ldsTooBig("bg_rt_kernel", lds, lim_);
-                hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, p, src, od, g);
+                hipLaunchKernelGGL((bg_rt_kernel<TC, NS>), gd, bd, lds, st, ka);
             } else {
-                hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, p, src, od, g);
+                hipLaunchKernelGGL((bg_rb_kernel<TC, NS>), gd, bd, 0, st, ka);
             }
             return hipGetLastError();
         }
@@ -1014,11 +1205,11 @@ static hipError_t bgDispatch(const BgDev& p, const SrcDesc& src, const OutDesc& 
     if (threads > bgMaxThreads(sizeof(TC) == 8, NS)) return hipErrorInvalidConfiguration;
     const bool single = g.kch == 1 && g.nprog <= g.nwt;  // one program per wave: A loaded once
     if (globalB) {
-        if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, true, true>), gd, bd, lds, st, p, src, od, g);
-        else hipLaunchKernelGGL((bg_kernel<TC, NS, true, false>), gd, bd, lds, st, p, src, od, g);
+        if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, true, true>), gd, bd, lds, st, ka);
+        else hipLaunchKernelGGL((bg_kernel<TC, NS, true, false>), gd, bd, lds, st, ka);
     } else {
-        if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, false, true>), gd, bd, lds, st, p, src, od, g);
-        else hipLaunchKernelGGL((bg_kernel<TC, NS, false, false>), gd, bd, lds, st, p, src, od, g);
+        if (single) hipLaunchKernelGGL((bg_kernel<TC, NS, false, true>), gd, bd, lds, st, ka);
+        else hipLaunchKernelGGL((bg_kernel<TC, NS, false, false>), gd, bd, lds, st, ka);
     }
     return hipGetLastError();
 }

@@ -201,12 +201,16 @@ void attachExact(const BgPlan& p, DevBuf& X, StageRT& s, BgDev& d, bool dry) {
     d.xT1 = s.d.dft.taps;
     d.xT2 = s.d.poly.taps;
     if (dry) return;
+    // [rows (f64) | rowInfo (int) | bg_kernel's fix list (kBgNfInts ints, zeroed)]
     const size_t nr = p.rows.size(), ni = p.rowInfo.size();
-    X.ensure(nr * 8 + ni * 4 + 16);
+    const size_t listOff = (nr * 8 + ni * 4 + 15) / 16 * 16;
+    X.ensure(listOff + kBgNfListBytes);
     HIPCHK(hipMemcpy(X.p, p.rows.data(), nr * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(static_cast<char*>(X.p) + nr * 8, p.rowInfo.data(), ni * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(static_cast<char*>(X.p) + listOff, 0, kBgNfListBytes));
     d.xRows = static_cast<const double*>(X.p);
     d.xInfo = reinterpret_cast<const int*>(static_cast<const char*>(X.p) + nr * 8);
+    d.nfList = reinterpret_cast<int*>(static_cast<char*>(X.p) + listOff);
     if (p.twoStage) {
         if (!s.xBankA.p) s.xBankA.upload(s.d.poly.a);
         if (!s.xBankC.p) s.xBankC.upload(s.d.dft.c);
@@ -1957,9 +1961,10 @@ void gar_reset(gar_resampler* r) {
         if (!r->dry) (void)devFault(r);  // a raised status word takes the recovery path (and is cleared there)
         if (r->poisoned) {  // recover: drain the handle's streams, fresh state
             // the failing call recorded no order event, and launches it already queued on its
-            // caller stream may still read the histories and scratch freed below: drain that stream
-            // (only the streams this handle enqueued on -- never the whole device; the failing call's
-            // stream through the event recorded on it, since the caller may have destroyed it)
+            // caller stream may still read the histories and scratch freed below: drain the failing
+            // call's stream through the event recorded on it (the caller may have destroyed it), then
+            // the earlier calls (drainOrder: their order event, or -- a handle used on one stream
+            // records none -- the whole device, gar.h gar_process_device)
             if (r->failEvValid) (void)hipEventSynchronize(r->failEv);
             if (r->stream) (void)hipStreamSynchronize(r->stream);
             drainOrder(r);

@@ -181,12 +181,6 @@ __device__ __forceinline__ void hxLoad(const HxArgs& x, const HxItems& it, int b
 // any dtype); rows >= W and columns past the launch are zero.  Out of line:
 // only the first and last blocks of a launch take it.
 typedef const __attribute__((address_space(4))) struct HxArgs* HxArgsP;
-template <class T>
-__device__ __forceinline__ T kload(const __attribute__((address_space(4))) T* p) {
-    T v;
-    __builtin_memcpy(&v, (const T*)p, sizeof(T));
-    return v;
-}
 
 __device__ __forceinline__ f32x4 hxGatherSlot(HxArgsP xp, int bl, int q, int row) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};

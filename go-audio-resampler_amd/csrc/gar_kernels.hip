@@ -252,9 +252,17 @@ hipError_t launchBg(const BgDev& p, const SrcDesc& src, const OutDesc& od, int C
                 p.f64, p.Pc, p.Qc, p.Kc, p.Kread, p.NS, g.kch, g.nwt, g.ncg, g.nprog, g.nred, g.nslots, g.G,
                 (long long)nmac, C, g.nblocks, (long long)blocks, lds, globalB ? 1 : 0, (long long)od.o_lo, (long long)od.o_hi);
     }
-    if (p.f64) return bgLaunchF64(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
-    if (p.NS < 56) return bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
-    return bgLaunchF32b(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
+    hipError_t e;
+    if (p.f64) e = bgLaunchF64(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
+    else if (p.NS < 56) e = bgLaunchF32a(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
+    else e = bgLaunchF32b(p.NS, p, src, od, g, threads, lds, blocks, stream, globalB);
+    if (e != hipSuccess || !p.nfList) return e;
+    // the outputs of blocks that staged a non-finite sample (bg_nf_kernel: returns at once when none did)
+    const BgArgs ka{p, src, od, g};
+    const dim3 ng(static_cast<unsigned>(std::max(1, std::min(g.nblocks, 256)))), nb(256);
+    if (p.f64) hipLaunchKernelGGL(bg_nf_kernel<double>, ng, nb, 0, stream, ka);
+    else hipLaunchKernelGGL(bg_nf_kernel<float>, ng, nb, 0, stream, ka);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

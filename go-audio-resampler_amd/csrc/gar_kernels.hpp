@@ -86,7 +86,9 @@ struct BgDev {
     int xRowMax, xTwoStage, xT1, xT2;
     const double* xPolyA;  // [L][T2]
     const double* xDftC;   // [2][T1]
+    int* nfList;           // bg_kernel's non-finite fix list (gar_bg.hpp kBgNfInts ints, zeroed)
 };
+constexpr size_t kBgNfListBytes = 4 * (2 + 256 * 129 + 1);  // gar_bg.hpp kBgNfInts (static_assert there)
 
 // Device copy of an HxPlan (gar_plan.hpp): split-f16 MFMA FIR, f32 compute.
 struct HxDev {

@@ -169,7 +169,13 @@ gar_status gar_flush_multi_f64(gar_resampler *r, double *const *out, int32_t n_c
  * stream); returns once the work is enqueued.  Calls on one handle are
  * ordered even across streams (each waits for the handle's previous call);
  * the caller keeps `in` alive and `out` untouched until `stream` has run the
- * call.  A device error leaves the handle refusing work (GAR_ERR_DEVICE)
+ * call.  Cost of that ordering: while a handle is used on ONE stream its calls
+ * record no event (an event costs ~3.5 us of stream time per call), so the
+ * first call on a different stream, gar_synchronize, gar_reset and gar_free
+ * wait with hipDeviceSynchronize -- every stream of the device, including
+ * other handles' work; do not call them while another thread captures a
+ * stream.  After the first switch every call records an event and these wait
+ * for that event only.  A device error leaves the handle refusing work (GAR_ERR_DEVICE)
  * until gar_reset.  The handle's device is made current for the call and the
  * caller's current device restored. */
 gar_status gar_process_device(gar_resampler *r, const void *in, int32_t in_dtype, int64_t in_frame_stride,
