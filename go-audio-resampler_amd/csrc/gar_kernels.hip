@@ -334,9 +334,22 @@ __global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc s
         const int64_t bhi = p.u_base + ((p.at0 + mhi * p.step) >> 16) / L + T;  // exclusive
         const int nr = static_cast<int>(bhi - blo);                              // <= winRows (launcher bound)
         __syncthreads();  // previous tile's window consumed
-        for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
-            const int r = e / C, c = e - r * C;
-            win[e] = same ? srcReadBF<TC>(src, blo + r, c, r < winRows, bankG) : srcRead<TC>(src, blo + r, c);
+        // interior tile (uniform): the window is nr consecutive whole rows of the input or of the
+        // history, [t][C] contiguous -> one plain coalesced copy (the general gather's 64-bit source
+        // selection per element was a third of the kernel's instructions, r06 ISA census)
+        const bool inWin = same && src.in && src.in_cs == 1 && src.in_fs == C && blo >= src.in_base &&
+                           bhi <= src.in_base + src.in_len && bhi <= src.valid_end && blo >= 0 && nr <= winRows;
+        const bool hWin = !inWin && same && src.hist && src.hist_ld == C && blo >= src.hist_base &&
+                          bhi <= src.hist_base + src.hist_len && bhi <= src.valid_end && blo >= 0 && nr <= winRows;
+        if (inWin || hWin) {
+            const TC* base = inWin ? static_cast<const TC*>(src.in) + (blo - src.in_base) * C
+                                   : static_cast<const TC*>(src.hist) + (blo - src.hist_base) * C;
+            for (int e = threadIdx.x; e < nr * C; e += blockDim.x) win[e] = base[e];
+        } else {
+            for (int e = threadIdx.x; e < nr * C; e += blockDim.x) {
+                const int r = e / C, c = e - r * C;
+                win[e] = same ? srcReadBF<TC>(src, blo + r, c, r < winRows, bankG) : srcRead<TC>(src, blo + r, c);
+            }
         }
         __syncthreads();
         if (i0 + threadIdx.x >= i1) continue;
@@ -362,6 +375,8 @@ __global__ __launch_bounds__(kPolyThreads) void poly_kernel(PolyDev p, SrcDesc s
         TC acc[CG];
 #pragma unroll
         for (int j = 0; j < CG; ++j) acc[j] = 0;
+        // (one loop of T taps with a wrap test: split at the wrap, the two loops' trip counts differ
+        // per lane and the wave runs the longest of each -- r06: 1.13 -> 1.58 ms)
         int k = polyRot(p.m0 + m, ph, T);
 #pragma unroll 8
         for (int i = 0; i < T; ++i) {
