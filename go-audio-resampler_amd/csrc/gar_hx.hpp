@@ -203,7 +203,28 @@ __device__ __forceinline__ f32x4 hxGatherSlot(HxArgsP xp, int bl, int q, int row
 // 2^-kHxLs, so a lo half stays normal whenever its hi half is: 22-bit
 // precision for every |v| >= 2^-(14+kHxXs)).  Scalar f32 VALU: packed f32
 // arithmetic next to MFMAs costs issue cycles.
-__device__ __forceinline__ void hxSplit2(float a, float b, uint32_t& hi, uint32_t& lo) {
+// GAR_HX_MIXSPLIT: the same halves from mixed-precision FMAs -- hi = f16(v*2^12) and
+// lo = f16((v*2^12 - hi)*2^11) each one v_fma_mix{lo,hi}_f16 (rounded once to f16, the product by a
+// power of two and the difference exact, as in the plain split), the difference one v_fma_mix_f32:
+// 6 VALU per pair instead of 8 (2 v_mul + v_cvt_pk, twice, + 2 v_fma_mix).  A -0 input gives a +0 hi
+// half here (-0 * 2^12 + 0), -0 in the plain split: no output changes (an MFMA sum that starts at +0).
+#ifndef GAR_HX_MIXSPLIT
+#define GAR_HX_MIXSPLIT 0
+#endif
+__device__ __forceinline__ void hxSplit2Mix(float a, float b, uint32_t& hi, uint32_t& lo) {
+    const float kS = static_cast<float>(1 << kHxXs), kL = static_cast<float>(1 << kHxLs);
+    uint32_t h, l;
+    float ra, rb;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(a), "s"(kS));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(b), "s"(kS));
+    asm("v_fma_mix_f32 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(ra) : "v"(a), "s"(kS), "v"(h));
+    asm("v_fma_mix_f32 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(rb) : "v"(b), "s"(kS), "v"(h));
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(l) : "v"(ra), "s"(kL));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(l) : "v"(rb), "s"(kL));
+    hi = h;
+    lo = l;
+}
+__device__ __forceinline__ void hxSplit2Plain(float a, float b, uint32_t& hi, uint32_t& lo) {
     const float sa = a * static_cast<float>(1 << kHxXs), sb = b * static_cast<float>(1 << kHxXs);
     const h2v h = __builtin_convertvector(f2v{sa, sb}, h2v);
     const float ra = (sa - static_cast<float>(h.x)) * static_cast<float>(1 << kHxLs);
@@ -211,6 +232,10 @@ __device__ __forceinline__ void hxSplit2(float a, float b, uint32_t& hi, uint32_
     const h2v l = __builtin_convertvector(f2v{ra, rb}, h2v);
     hi = __builtin_bit_cast(uint32_t, h);
     lo = __builtin_bit_cast(uint32_t, l);
+}
+__device__ __forceinline__ void hxSplit2(float a, float b, uint32_t& hi, uint32_t& lo) {
+    if constexpr (GAR_HX_MIXSPLIT) hxSplit2Mix(a, b, hi, lo);
+    else hxSplit2Plain(a, b, hi, lo);
 }
 
 __device__ __forceinline__ bool hxLoud(float v) { return !(__builtin_fabsf(v) < kHxLoud); }

@@ -48,6 +48,12 @@ constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
 #ifndef GAR_HXT_LPRIO
 #define GAR_HXT_LPRIO 0
 #endif
+// development: attribution modes compiled into a production build (the GAR_HXS_DBG bits, outputs
+// wrong by design) -- the runtime knob needs the GAR_HXS_DEV build, whose stamps and knob loads
+// change the kernel being attributed (r06t: 2.28 vs 1.70 ms on ns256)
+#ifndef GAR_HXT_CTDBG
+#define GAR_HXT_CTDBG 0
+#endif
 constexpr uint32_t kHxtLoudBits = 0x417FF000u;          // bits(kHxLoud = 15.99609375f): !(|x| < kHxLoud) <=> (bits & 0x7fffffff) >= it
 static_assert(__builtin_bit_cast(uint32_t, kHxLoud) == kHxtLoudBits, "hxt's loud test must match hxLoud");
 
@@ -116,6 +122,14 @@ __device__ __forceinline__ void hxtPut(char* qb, uint32_t dL, int p, int R, int 
 }
 
 __device__ __forceinline__ uint32_t hxtMag(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+// GAR_HXT_HILOUD: the loud test read off the f16 hi halves instead of the f32 inputs -- !(|x| < kHxLoud)
+// (NaN included) <=> x * 2^12 >= 65520 in magnitude or NaN <=> its f16 rounding is Inf / NaN <=>
+// (hi & 0x7fff) >= 0x7c00 (65520 ties to even, i.e. to Inf; hxSplit2).  One v_and + one v_pk_max_u16
+// per two elements instead of an and + a max per element.
+#ifndef GAR_HXT_HILOUD
+#define GAR_HXT_HILOUD 0
+#endif
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
 
 // (r05: the split with v_pk_mul_f32 for the two power-of-two scalings -- 12 instead of 16 VALU per
 // item -- measured slower on every workload, ns256 1.766 vs 1.732 ms, cfg3 0.332 vs 0.317 ms: packed f32
@@ -211,6 +225,7 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
     int ln = lane, lq = l;
     asm volatile("" : "+v"(ln), "+s"(lq));
     uint32_t m = 0;
+    u16x2v mh = {0, 0};  // GAR_HXT_HILOUD: running max of the hi halves' magnitude bits
     auto itemPos = [&](int k, int& row, int& q) {  // -> whether item k holds rows of this load (uniform)
         if constexpr (FMT == 1) {
             const int it = lq + NL * k, pc = it >> 2;
@@ -235,9 +250,14 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
         for (int u = 0; u < kSplitChunk; ++u) {  // items the load does not hold were loaded as zeros
             if (k0 + u >= K) break;
             const f32x4 e = hxtItem<FMT, NL>(r, k0 + u);
-            m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
+            if constexpr (!GAR_HXT_HILOUD)
+                m = max(m, max(max(hxtMag(e[0]), hxtMag(e[1])), max(hxtMag(e[2]), hxtMag(e[3]))));
             hxSplit2(e[0], e[1], hv[u].x, lv[u].x);
             hxSplit2(e[2], e[3], hv[u].y, lv[u].y);
+            if constexpr (GAR_HXT_HILOUD) {
+                mh = __builtin_elementwise_max(mh, __builtin_bit_cast(u16x2v, hv[u].x & 0x7fff7fffu));
+                mh = __builtin_elementwise_max(mh, __builtin_bit_cast(u16x2v, hv[u].y & 0x7fff7fffu));
+            }
         }
 #pragma unroll
         for (int u = 0; u < kSplitChunk; ++u) {
@@ -273,7 +293,8 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
         }
     }
 #endif
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(m >= kHxtLoudBits) != 0, 0))
+    const bool loud = GAR_HXT_HILOUD ? (mh.x >= 0x7c00u || mh.y >= 0x7c00u) : m >= kHxtLoudBits;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(loud) != 0, 0))
         hxtLoudLoad<FMT, NL>(hxsCold(), st, b, l, lane, sh);
 }
 
@@ -434,7 +455,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     const int GQ = x.G * x.Qc, Wg = x.Wg, R = x.R;
     const int P = (Wg + GQ - 1) / GQ, nL = P + x.ngroups - 1;
     const int nstepsPad = hxsStepsPad(x);
-    const int dbg = kHxsDev ? x.dbg : 0;
+    const int dbg = kHxsDev ? x.dbg : GAR_HXT_CTDBG;
     // per block (uniform): loads go through the buffer records ("fast") when every column of the
     // block is live and the load's first row lies at or after the raw input's first row
     const int c1 = b * 16 + 15;
@@ -523,7 +544,7 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
     const int GQ = x.G * x.Qc;
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
     const uint32_t pst = 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(ro.st);
-    const int dbg = kHxsDev ? x.dbg : 0;
+    const int dbg = kHxsDev ? x.dbg : GAR_HXT_CTDBG;
     auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
         const f32x4 y = hxScale(oA, oL, sh);
         if (dbg & 2) return;

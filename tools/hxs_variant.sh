@@ -6,7 +6,7 @@
 set -e
 name=$1; flags=$2
 cd "$(dirname "$0")/../go-audio-resampler_amd"
-make -s -j8 >/dev/null
+[ -n "$SKIPMAKE" ] || make -s -j8 >/dev/null
 mkdir -p build/$name
 CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -fno-slp-vectorize -I../include -Icsrc -I/opt/rocm/include"
 units=${UNITS:-"gar_hxs gar_hxs_i1 gar_hxs_i2 gar_hxt_i1 gar_hxt_i2"}
