@@ -96,6 +96,7 @@ hipError_t hxtFmtL(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st)
     if (x.fmt == 1 && x.vst == 2) return hxtLaunch<NS, 1, 2, NL>(x, lds, blocks, st);
     if (x.fmt == 2 && x.vst == 0) return hxtLaunch<NS, 2, 0, NL>(x, lds, blocks, st);
     if (x.fmt == 2 && x.vst == 1) return hxtLaunch<NS, 2, 1, NL>(x, lds, blocks, st);
+    if (x.fmt == 5 && x.vst == 0) return hxtLaunch<NS, 5, 0, NL>(x, lds, blocks, st);
     return hipErrorNotSupported;
 }
 template <int NS>
@@ -149,6 +150,9 @@ hipError_t hxsVst(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t st) 
 // progress counters (kHxtSyncOff + kHxtSyncBytes, rounded up).
 static_assert(kHxtSyncOff + kHxtSyncBytes <= 320, "hxt progress counters past the reserved LDS");
 static size_t hxsLds(int Rt) { return 4 * (16 * static_cast<size_t>(Rt) + 64) + 320; }
+// hxt_kernel FMT 5 (32-channel blocks): eight quads, loudLo/Hi[32] + flag + the progress counters
+static_assert(288 + kHxtSyncBytes <= 448, "hxt FMT 5 progress counters past the reserved LDS");
+static size_t hxtLdsWide(int Rt) { return 8 * (16 * static_cast<size_t>(Rt) + 64) + 448; }
 
 // Ring geometry of G periods per group: R ring rows, Rt rows incl. the mirror (rounded to 16 so
 // the quad stride 16*Rt + 64 is 64 mod 256 B: the four quads of a transposed read land on
@@ -183,6 +187,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
     static const int knobWg = std::getenv("GAR_HXS_WGPERCU") ? std::atoi(std::getenv("GAR_HXS_WGPERCU")) : 0;
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
+    static const int knobWide = std::getenv("GAR_HXT_WIDE") ? std::atoi(std::getenv("GAR_HXT_WIDE")) : 1;
     static const int knobDbg = std::getenv("GAR_HXS_DBG") ? std::atoi(std::getenv("GAR_HXS_DBG")) : 0;
     const int64_t Pc = p.Pc, Qc = p.Qc;
     const int64_t a_lo = fdiv(od.o_lo, Pc), a_hi = cdiv(od.o_hi, Pc);
@@ -194,9 +199,15 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     // window gathered in one pass -- latency over bandwidth (knob GAR_HXS_SMALL=0/1 forces)
     static const int knobSmall = std::getenv("GAR_HXS_SMALL") ? std::atoi(std::getenv("GAR_HXS_SMALL")) : -1;
     const bool small = knobSmall >= 0 ? knobSmall == 1 : nmac * C <= static_cast<int64_t>(16) * 2 * ncu;
-    // chunk length: about one block (16 columns) per CU
+    // 32-channel blocks of f32 rows on hxt_kernel (FMT 5, gar_hxt.hpp): whole 128-B lines per load and
+    // store instruction; decided here (the chunk count depends on the block width), confirmed below
+    const uintptr_t inA0 = reinterpret_cast<uintptr_t>(src.in);
+    bool wide = knobWide != 0 && !small && src.in && !src.in_pcm && !src.in_f64 && !od.pcm && !od.f64 && C % 32 == 0 &&
+                (inA0 & 15) == 0 && src.in_cs == 1 && src.in_fs % 4 == 0 && p.rb && p.nw <= kHxRbMaxWaves;
+    const int bw = wide ? 32 : 16;
+    // chunk length: about one block (bw columns) per CU
     const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
-    const int64_t nchunkT = small ? nmac : std::max<int64_t>(1, (targetBlocks * 16 + C - 1) / C);
+    const int64_t nchunkT = small ? nmac : std::max<int64_t>(1, (targetBlocks * bw + C - 1) / C);
     int64_t Np = std::max<int64_t>(1, cdiv(nmac, nchunkT));
     static const int knobNp = std::getenv("GAR_HXS_NP") ? std::atoi(std::getenv("GAR_HXS_NP")) : 0;
     if (knobNp > 0 && !small) Np = knobNp;  // development: chunk length in macro periods
@@ -258,6 +269,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     bool hxt = knobHxt != 0 && !small && !od.pcm && !od.f64 && !src.in_pcm &&
                ((fmt == 1 && vst == 2) || (fmt == 2 && (vst == 0 || vst == 1)));
     if (hxt) ncomp = hxtRoles(p.nw, p.NS, role, &maxStride);
+    wide = wide && hxt && fmt == 2 && vst == 0;
+    if (wide) fmt = 5;
 
     int G = 0, R = 0, Rt = 0, Wg = 0;
     auto pickG = [&]() {
@@ -267,8 +280,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
                 hxsRingFor(p, cand, r, rt, wg);
                 if (cand > 1 && cand > Np) continue;
                 if (knobG > 0 && cand > knobG && cand > 1) continue;
-                if (!hxsRingFits(p, cand, rt)) continue;
-                if (hxt && cand * Qc > hxtMaxRows(ncomp + 6 <= kHxtWaves ? 6 : 4)) continue;
+                if (fmt == 5 ? hxtLdsWide(rt) > 160 * 1024 : !hxsRingFits(p, cand, rt)) continue;
+                if (hxt && cand * Qc > hxtMaxRowsF(fmt, ncomp + 6 <= kHxtWaves ? 6 : 4)) continue;
                 // hxt: a producer runs at most (ring slots + 2) loads / groups ahead of the slowest one,
                 // which the arrival slots must cover (gar_hxt.hpp progress counters)
                 if (hxt && r / (cand * static_cast<int>(Qc)) + 3 > kHxtSlots) continue;
@@ -279,6 +292,14 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         }
     };
     pickG();
+    // a 32-channel ring holds half the rows: keep it only with groups of >= 2 periods and one compute
+    // wave per row block (r06y / r06z: cfg3, NS = 10 on balanced roles at G = 2, lost 4-12 % -- its
+    // chunks halve, traffic / algorithmic 1.06 -> 1.12), else 16-channel blocks
+    if (fmt == 5 && (G < 2 || maxStride > 1)) {
+        fmt = 2;
+        G = 0;
+        pickG();
+    }
     if (G == 0 && hxt) {  // no group size fits hxt_kernel's limits: hxs_kernel's
         hxt = false;
         ncomp = 0;
@@ -295,7 +316,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     x.Pc = p.Pc; x.Qc = p.Qc; x.Kc = p.Kc; x.Kread = p.Kread; x.G = G; x.C = C;
     x.nprog = p.nw;
     x.ncols = static_cast<int>(ncols);
-    x.nblocks = static_cast<int>((ncols + 15) / 16);
+    x.nblocks = static_cast<int>(fmt == 5 ? (ncols + 31) / 32 : (ncols + 15) / 16);
     x.Np = static_cast<int>(Np);
     x.ngroups = static_cast<int>(cdiv(Np, G));
     x.R = R; x.Rt = Rt; x.mirror = std::max(0, Wg - G * static_cast<int>(Qc)); x.Wg = Wg;
@@ -410,7 +431,7 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
         x.R = R; x.Rt = Rt; x.mirror = 0;
     }
     if (trace && x.qGroups > 0) fprintf(stderr, "hxq: qRbs=%d qGroups=%d workgroups=%lld\n", x.qRbs, x.qGroups, (long long)x.nblocks * x.qGroups);
-    const size_t lds = hxsLds(Rt);
+    const size_t lds = fmt == 5 ? hxtLdsWide(Rt) : hxsLds(Rt);
     const int64_t blocks = x.nblocks;
     if (hxt) {
         const int64_t hblocks = blocks;

@@ -385,13 +385,16 @@ struct HxsRegSrc {
 template <int FMT, class XP>
 __device__ __forceinline__ HxsRegSrc hxsRegSrc(XP x, int b, int lane) {
     HxsRegSrc r;
-    const int col0 = b * 16, k = col0 / x->C, c0 = col0 - k * x->C;
+    const int col0 = b * (FMT == 5 ? 32 : 16), k = col0 / x->C, c0 = col0 - k * x->C;
     r.rowB = static_cast<int>(x->in_fs) * x->in_esz;
     r.chunkB = x->Np * x->Qc * r.rowB;
-    r.r = hxsRsrcT(x, hxsChunkRow(x, k, 0), FMT == 2 ? c0 : 0, FMT == 2 ? 64 : (FMT == 3 ? 4 : 8));
+    r.r = hxsRsrcT(x, hxsChunkRow(x, k, 0), (FMT == 2 || FMT == 5) ? c0 : 0,
+                   FMT == 5 ? 128 : FMT == 2 ? 64 : (FMT == 3 ? 4 : 8));
     // ROW16: lane = 16 q + r reads row r of a 16-row piece, channels 4q..4q+3 -- one instruction
-    // covers 16 whole 64-B block rows (16 lines) instead of 16 B of 64 rows (64 lines)
-    r.lane0 = FMT == 2 ? (lane & 15) * r.rowB + 16 * (lane >> 4) : lane * r.rowB;
+    // covers 16 whole 64-B block rows (16 lines) instead of 16 B of 64 rows (64 lines); ROW32 (FMT 5,
+    // hxt_kernel only): lane = 8 r + q, 8 whole 128-B rows per instruction
+    r.lane0 = FMT == 5 ? (lane >> 3) * r.rowB + 16 * (lane & 7)
+            : FMT == 2 ? (lane & 15) * r.rowB + 16 * (lane >> 4) : lane * r.rowB;
     return r;
 }
 

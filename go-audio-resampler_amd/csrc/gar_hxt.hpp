@@ -35,9 +35,20 @@ constexpr int kHxtD = 2;                                // loads in flight per l
 __host__ __device__ constexpr int hxtPieces(int NL) { return NL >= 6 ? 12 : 10; }
 __host__ __device__ constexpr int hxtMaxRows(int NL) { return 64 * hxtPieces(NL); }
 // Items of loader l (of NL): FMT 1 item it = l + NL*k covers quad it & 3, 64-row piece it >> 2;
-// FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row).
+// FMT 2 item it = l + NL*k is the 16-row piece it (all four quads, lane = 16 quad + row);
+// FMT 5 item it is the 8-row piece it of a 32-channel block (all eight quads, lane = 8 row + quad).
 template <int NL>
 constexpr int hxtItems() { return (4 * hxtPieces(NL) + NL - 1) / NL; }
+// FMT 5 (round 6): 32-channel blocks of f32 rows -- every load and store instruction of a workgroup
+// covers whole 128-B lines (tools/ubench/row16_copy: the ns256 memory pattern with 64-B half rows per
+// workgroup runs at 3.0 TB/s with no compute at all, 1.86 ms; with 128-B rows 4.0-4.2 TB/s, 1.36-1.40
+// ms).  The block is two 16-column tiles (sub-blocks 2b, 2b+1 of the 16-column numbering) over one
+// ring of eight quads; each compute wave runs both tiles of its row block per period.
+__host__ __device__ constexpr int hxtQuads(int FMT) { return FMT == 5 ? 8 : 4; }
+__host__ __device__ constexpr int hxtCols(int FMT) { return 4 * hxtQuads(FMT); }
+__host__ __device__ constexpr int hxtMaxRowsF(int FMT, int NL) {
+    return FMT == 5 ? 8 * NL * ((4 * hxtPieces(NL) + NL - 1) / NL) : 64 * hxtPieces(NL);
+}
 // loader waves' issue priority (s_setprio; 0 = the compute waves' level).  The loaders share each
 // SIMD with three MFMA-issuing compute waves; at equal priority the arbiter lets the MFMA stream
 // starve the loaders' VALU (r05 stamps: ~19 cycles per loader VALU instruction), and the loaders
@@ -76,6 +87,10 @@ template <int NL>
 struct HxtBuf<2, NL> {  // 16-channel f32 rows: four channels of one row per lane
     f32x4 v[hxtItems<NL>()];
 };
+template <int NL>
+struct HxtBuf<5, NL> {  // 32-channel f32 rows: four channels of one row per lane
+    f32x4 v[hxtItems<NL>()];
+};
 
 // Issue load `st` (a real load when live and fast; otherwise every item's offset lies past the
 // records, which returns zeros without a memory access -- the same instruction pattern on every
@@ -98,10 +113,11 @@ __device__ __forceinline__ bool hxtIssue(const HxsStage& st, bool live, const Hx
             const int o2 = on ? o + chunkB : o;
             r.a[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o, 0, 0));
             r.b[k] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
-        } else {  // 16-row piece l + NL k, lane = 16 quad + row
+        } else {  // FMT 2: 16-row piece l + NL k, lane = 16 quad + row; FMT 5: 8-row piece, lane = 8 row + quad
+            constexpr int kRp = FMT == 5 ? 8 : 16;
             const int it = lq + NL * k;
-            const bool on = 16 * it < nrow;
-            const int o = on ? base + 16 * it * rowB : static_cast<int>(0x80000000u);
+            const bool on = kRp * it < nrow;
+            const int o = on ? base + kRp * it * rowB : static_cast<int>(0x80000000u);
             r.v[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
         }
     }
@@ -162,6 +178,11 @@ __device__ GAR_HXT_SLOW_ATTR void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, i
             if (pc >= hxtPieces(NL) || 64 * pc >= st.nrow) continue;
             row = 64 * pc + lane;
             q = it & 3;
+        } else if constexpr (FMT == 5) {
+            const int it = l + NL * k;
+            if (8 * it >= st.nrow) break;
+            row = 8 * it + (lane >> 3);
+            q = lane & 7;
         } else {
             const int it = l + NL * k;
             if (16 * it >= st.nrow) break;
@@ -172,7 +193,7 @@ __device__ GAR_HXT_SLOW_ATTR void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, i
         f32x4 e;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const int col = b * 16 + 4 * q + n;
+            const int col = b * hxtCols(FMT) + 4 * q + n;
             const int kk = col / xp->C, c = col - kk * xp->C;
             e[n] = hxsGather(src, hxsChunkRow(xp, kk, st.T0 + row), c, xp->A);
         }
@@ -183,17 +204,18 @@ __device__ GAR_HXT_SLOW_ATTR void hxtLoudLoad(HxsArgsP xp, HxsStage st, int b, i
 // Edge load (rows before the raw input, partial blocks, any other layout): every element gathered
 // through the SrcDesc (history | input | zeros); out of line.  Loader l takes items l, l+4, ...
 // of the 4 quads x ceil(nrow/64) pieces.
+template <int NQ>
 __device__ GAR_HXT_SLOW_ATTR void hxtGatherLoad(HxsArgsP xp, HxsStage st, int b, int l, int nl, int lane, HxsShared sh) {
     const SrcDesc src = kload(&xp->src);
     const int p0 = uni(st.T0 % xp->R);
-    const int nit = 4 * ((st.nrow + 63) >> 6);
+    const int nit = NQ * ((st.nrow + 63) >> 6);
     for (int it = l; it < nit; it += nl) {
-        const int q = it & 3, row = 64 * (it >> 2) + lane;
+        const int q = it % NQ, row = 64 * (it / NQ) + lane;
         if (row >= st.nrow) continue;
         f32x4 e;
 #pragma unroll
         for (int n = 0; n < 4; ++n) {
-            const int col = b * 16 + 4 * q + n;
+            const int col = b * 4 * NQ + 4 * q + n;
             const int kk = col / xp->C, c = col - kk * xp->C;
             e[n] = col < xp->ncols ? hxsGather(src, hxsChunkRow(xp, kk, st.T0 + row), c, xp->A) : 0.f;
         }
@@ -232,6 +254,11 @@ __device__ __forceinline__ void hxtConvert(const HxsArgs& x, const HxsStage& st,
             row = 64 * pc + ln;
             q = it & 3;
             return pc < hxtPieces(NL) && 64 * pc < nrow;
+        } else if constexpr (FMT == 5) {
+            const int it = lq + NL * k;
+            row = 8 * it + (ln >> 3);
+            q = ln & 7;
+            return 8 * it < nrow;
         } else {
             const int it = lq + NL * k;
             row = 16 * it + (ln & 15);
@@ -328,7 +355,9 @@ struct HxtSync {
     lds_i32* abort;   // a wait of this workgroup expired (sticky for the launch)
 };
 // LDS bytes past loudLo (hxsLds reserves them): loudLo[16], loudHi[16], flag, then the counters
+// (FMT 5: loudLo[32], loudHi[32], flag)
 constexpr int kHxtSyncOff = 160;
+__host__ __device__ constexpr int hxtSyncOff(int FMT) { return FMT == 5 ? 288 : kHxtSyncOff; }
 constexpr int kHxtSyncBytes = 4 * (2 * kHxtSlots + 1);
 
 // Producer arrival for item j.
@@ -388,8 +417,9 @@ __device__ __forceinline__ int hxtFreeNeed(const HxsArgs& x, int j, int P) {
 // Block b's first window (rows [0, Wg), i.e. loads 0 .. P-1) can come through the buffer records
 // (uniform): every column live and the window at or after the raw input's first row.
 __device__ __forceinline__ bool hxtStage0Fast(const HxsArgs& x, int b) {
-    const bool blockLive = x.fmt >= 1 && x.fmt <= 2 && b * 16 + 15 < x.ncols && x.fastHi > x.fastLo;
-    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * 16) / x.C) * x.Np) * x.Qc;
+    const int W = x.fmt == 5 ? 32 : 16;
+    const bool blockLive = (x.fmt == 1 || x.fmt == 2 || x.fmt == 5) && b * W + W - 1 < x.ncols && x.fastHi > x.fastLo;
+    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * W) / x.C) * x.Np) * x.Qc;
     return blockLive && row0 >= x.fastLo;
 }
 
@@ -411,7 +441,7 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
     st.nrow = x.Wg;
     st.fast = true;
     const int Wg = x.Wg;
-    const int nit = FMT == 1 ? 4 * ((Wg + 63) >> 6) : (Wg + 15) >> 4;
+    const int nit = FMT == 1 ? 4 * ((Wg + 63) >> 6) : FMT == 5 ? (Wg + 7) >> 3 : (Wg + 15) >> 4;
     bool met = !kOrdered;
     for (int it0 = w; it0 < nit; it0 += kCoopB * nw) {
         f32x4 e[kCoopB];
@@ -427,7 +457,7 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
                 const f2v c = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs.r, o2, 0, 0));
                 e[u] = f32x4{a.x, a.y, c.x, c.y};
             } else {
-                const int o = on ? rs.lane0 + 16 * it * rs.rowB : kHxqOob;
+                const int o = on ? rs.lane0 + (FMT == 5 ? 8 : 16) * it * rs.rowB : kHxqOob;
                 e[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs.r, o, 0, 0));
             }
         }
@@ -439,8 +469,8 @@ __device__ __forceinline__ void hxtCoopStage0(const HxsArgs& x, const HxsShared&
         for (int u = 0; u < kCoopB; ++u) {
             const int it = it0 + u * nw;
             if (it >= nit) continue;  // uniform
-            const int q = FMT == 1 ? (it & 3) : (lane >> 4);
-            const int row = FMT == 1 ? 64 * (it >> 2) + lane : 16 * it + (lane & 15);
+            const int q = FMT == 1 ? (it & 3) : FMT == 5 ? (lane & 7) : (lane >> 4);
+            const int row = FMT == 1 ? 64 * (it >> 2) + lane : FMT == 5 ? 8 * it + (lane >> 3) : 16 * it + (lane & 15);
             if (row < Wg) hxsPutItem(xp, st, 0, q, row, e[u], sh.ring, sh.QS, sh.loudLo, sh.loudHi, sh.flag);
         }
     }
@@ -458,9 +488,9 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     const int dbg = kHxsDev ? x.dbg : GAR_HXT_CTDBG;
     // per block (uniform): loads go through the buffer records ("fast") when every column of the
     // block is live and the load's first row lies at or after the raw input's first row
-    const int c1 = b * 16 + 15;
-    const bool blockLive = x.fmt >= 1 && x.fmt <= 4 && c1 < x.ncols && x.fastHi > x.fastLo;
-    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * 16) / x.C) * x.Np) * x.Qc;  // column-relative row 0
+    const int c1 = b * hxtCols(FMT) + hxtCols(FMT) - 1;
+    const bool blockLive = x.fmt >= 1 && x.fmt <= 5 && c1 < x.ncols && x.fastHi > x.fastLo;
+    const int64_t row0 = (x.a_lo + static_cast<int64_t>((b * hxtCols(FMT)) / x.C) * x.Np) * x.Qc;  // column-relative row 0
     const int64_t fastLo = x.fastLo;
     auto stage = [&](int j) {  // load j: the P parts of stage 0, then stages 1 ..
         HxsStage st;
@@ -516,7 +546,7 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
                 if (!((dbg & 16) && j >= P)) {
                     const HxsStage st = stage(j);
                     if (fastL[d]) hxtConvert<FMT, NL>(x, st, uni(p0), buf[d], b, l, lane, sh);
-                    else hxtGatherLoad(xp, st, b, l, NL, lane, sh);
+                    else hxtGatherLoad<hxtQuads(FMT)>(xp, st, b, l, NL, lane, sh);
                 }
                 unsigned long long t3 = stp ? __builtin_amdgcn_s_memtime() : 0;
                 if (stp) waited[4] += t3 - t1;
@@ -534,7 +564,9 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
 // Group g: wait for its window, run this wave's periods p = first, first + st, ... < end
 // (chunk-relative), publish.  One accumulator pair per period: with three compute waves per SIMD
 // the other waves cover a period's MFMA drain before its epilogue.
-template <int NS, int VST, bool FAST>
+// NT tiles per period (FMT 5: 2, the block's two 16-column halves, quads 4h .. 4h+3 of the ring and
+// channels ccol + 16h of the output; one accumulator pair per tile and period, in tile order).
+template <int NS, int VST, bool FAST, int NT = 1>
 __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_, const HxtSync& sy, int wt, int lane,
                                           const h8v (&Ah)[NS], const h8v (&Al)[NS], uint32_t laneOff, int u0, int P,
                                           int nslot, const HxtRole& ro, char* obase, int64_t pstride, int64_t aCol,
@@ -545,24 +577,27 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
     const uint32_t dL = 8u * static_cast<uint32_t>(x.Rt);
     const uint32_t pst = 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(ro.st);
     const int dbg = kHxsDev ? x.dbg : GAR_HXT_CTDBG;
-    auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p) {
+    const uint32_t tileLds = 4u * sh_.QS;                             // ring bytes between tiles
+    const int64_t tileOut = 16 * x.out_cs;                             // output bytes between tiles
+    auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p, int h) {
         const f32x4 y = hxScale(oA, oL, sh);
         if (dbg & 2) return;
         if constexpr (FAST) {
-            hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride, y, lane);
+            hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride + h * tileOut, y, lane);
         } else {
+            const int ccol_ = ccol + 16 * h;
             const int64_t a = aCol + p;
             const int64_t o0 = a * x.Pc + oRow0;
             const bool live = colOk && a < x.a_hi;
             if (fullRb && live && a * x.Pc >= x.o_lo && (a + 1) * x.Pc <= x.o_hi) {
-                char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol * x.out_cs);
+                char* pp = x.out + (o0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs + (VST == 2 ? 0 : ccol_ * x.out_cs);
                 hxsStoreFast<VST>(x, pp, y, lane);
             } else if (live) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int64_t o = o0 + i;
                     if (oRow0 + i < x.Pc && o >= x.o_lo && o < x.o_hi)
-                        *reinterpret_cast<float*>(x.out + o * x.out_fs + ccol * x.out_cs) = y[i];
+                        *reinterpret_cast<float*>(x.out + o * x.out_fs + ccol_ * x.out_cs) = y[i];
                 }
             }
         }
@@ -589,13 +624,16 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
                           8u * static_cast<uint32_t>((g % nslot) * GQ) + 8u * static_cast<uint32_t>(x.Qc) * static_cast<uint32_t>(first - p0);
             h8v bh0 = (dbg & 8) ? h8v{} : bFragA(aH), bl0 = (dbg & 8) ? h8v{} : bFragA(aH + dL);  // development 8: no B reads
             for (int i = 0; i < n; ++i) {
+#pragma unroll
+              for (int h = 0; h < NT; ++h) {
                 asm volatile("" : "+v"(aH));  // opaque per-period base: reads use base + offset:imm
-                const bool last = i + 1 == n;
+                const bool last = i + 1 == n && h + 1 == NT;
                 uint32_t aL = aH + dL;
 #if GAR_HXT_LOBASE
                 asm volatile("" : "+v"(aL));  // lo-row base kept apart: lo reads use aL + offset:imm (no per-step add of dL)
 #endif
-                const uint32_t aN = aH + pst, aNL = aN + dL;
+                // next tile: the other half of this period, or the next period's first tile
+                const uint32_t aN = h + 1 < NT ? aH + tileLds : aH - (NT - 1) * tileLds + pst, aNL = aN + dL;
                 f32x4 nA = {0, 0, 0, 0}, nL = nA;
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
@@ -616,8 +654,9 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
                     __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                epilogue(nA, nL, first + i * ro.st);
+                epilogue(nA, nL, first + i * ro.st, h);
                 aH = aN;
+              }
             }
         }
         const unsigned long long ta = (kHxsDev && st) ? __builtin_amdgcn_s_memtime() : 0;
@@ -658,7 +697,7 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
     const int nslot = x.R / GQ;
     const int P = (x.Wg + GQ - 1) / GQ;
     const int64_t pstride = static_cast<int64_t>(x.Pc) * x.out_fs;
-    const int col = b * 16 + l16;
+    const int col = b * hxtCols(FMT) + l16;  // FMT 5: tile 0's column (tile 1: + 16, the same chunk as C % 32 == 0)
     const bool colOk = col < x.ncols;
     const int kcol = col / x.C, ccol = col - kcol * x.C;
     const int64_t aCol = x.a_lo + static_cast<int64_t>(kcol) * x.Np;
@@ -667,12 +706,13 @@ __device__ __forceinline__ void hxtCompute(const HxsArgs& x, const HxsShared& sh
                           (aCol + x.Np) * x.Pc <= x.o_hi;
     char* obase = x.out + (aCol * x.Pc + oRow0 + ((VST == 2 && (lane & 1)) ? 2 : 0)) * x.out_fs +
                   (VST == 2 ? 0 : ccol * x.out_cs);
+    constexpr int NT = FMT == 5 ? 2 : 1;
     if (__builtin_amdgcn_ballot_w64(!laneFast) == 0)
-        hxtGroups<NS, VST, true>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                 colOk, ccol, fullRb, nl, st);
+        hxtGroups<NS, VST, true, NT>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
+                                     colOk, ccol, fullRb, nl, st);
     else
-        hxtGroups<NS, VST, false>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
-                                  colOk, ccol, fullRb, nl, st);
+        hxtGroups<NS, VST, false, NT>(x, sh_, sy, wt, lane, Ah, Al, laneOff, u0, P, nslot, ro, obase, pstride, aCol, oRow0,
+                                      colOk, ccol, fullRb, nl, st);
 }
 
 // FMT: 1 stereo f32 frames, 2 rows of 16 f32 channels.  VST: 0 any f32 layout, 1 channel-contiguous
@@ -684,12 +724,13 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     s.stamp = nullptr;
     s.QS = 16u * static_cast<uint32_t>(x.Rt) + 64u;  // quad: hi rows, lo rows, +64 B skew
     s.ring = reinterpret_cast<char*>(smem);
-    s.loudLo = reinterpret_cast<int*>(smem + 4 * static_cast<size_t>(s.QS));  // 16-B aligned (QS % 16 == 0)
-    s.loudHi = s.loudLo + 16;
-    s.flag = s.loudHi + 16;
+    constexpr int NQ = hxtQuads(FMT), NC = hxtCols(FMT);
+    s.loudLo = reinterpret_cast<int*>(smem + NQ * static_cast<size_t>(s.QS));  // 16-B aligned (QS % 16 == 0)
+    s.loudHi = s.loudLo + NC;
+    s.flag = s.loudHi + NC;
     HxtSync sy;
-    // kHxtSyncOff B past loudLo (hxsLds reserves the space past the ring): arrival slots, done counters, abort
-    sy.ldArr = (lds_i32*)(smem + 4 * static_cast<size_t>(s.QS) + kHxtSyncOff);
+    // kHxtSyncOff(FMT) B past loudLo (hxsLds reserves the space past the ring): arrival slots, done counters, abort
+    sy.ldArr = (lds_i32*)(smem + NQ * static_cast<size_t>(s.QS) + hxtSyncOff(FMT));
     sy.cpArr = sy.ldArr + kHxtSlots;
     sy.abort = sy.cpArr + kHxtSlots;
     const int lane = threadIdx.x & 63;
@@ -705,7 +746,7 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
         const int b = hxsBlock(x, bi);
         __syncthreads();  // the previous block's ring reads and fixup done
-        if (threadIdx.x < 16) {
+        if (threadIdx.x < NC) {
             s.loudLo[threadIdx.x] = INT_MAX;
             s.loudHi[threadIdx.x] = -1;
         }
@@ -725,7 +766,8 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
         if (*s.flag) {  // uniform
             __builtin_amdgcn_s_waitcnt(0);  // this wave's output stores landed
             __syncthreads();
-            hxsFixup(hxsCold(), b, s.loudLo, s.loudHi);
+            hxsFixup(hxsCold(), (NC / 16) * b, s.loudLo, s.loudHi);
+            if constexpr (NC == 32) hxsFixup(hxsCold(), 2 * b + 1, s.loudLo + 16, s.loudHi + 16);
         }
     }
     if (x.hn > 0) hxsHistKeep(x, static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x,
@@ -768,7 +810,8 @@ hipError_t hxtLaunch(const HxsArgs& x, size_t lds, int64_t blocks, hipStream_t s
     return hipGetLastError();
 }
 
-#define GAR_HXT_FOR3(M, NS) M(NS, 1, 2, 4) M(NS, 2, 0, 4) M(NS, 2, 1, 4) M(NS, 1, 2, 6) M(NS, 2, 0, 6) M(NS, 2, 1, 6)
+#define GAR_HXT_FOR3(M, NS) M(NS, 1, 2, 4) M(NS, 2, 0, 4) M(NS, 2, 1, 4) M(NS, 1, 2, 6) M(NS, 2, 0, 6) M(NS, 2, 1, 6) \
+    M(NS, 5, 0, 4) M(NS, 5, 0, 6)
 #if GAR_HXS_QUICK
 #define GAR_HXT_FOR_A(M) GAR_HXT_FOR3(M, 9)
 #define GAR_HXT_FOR_B(M) GAR_HXT_FOR3(M, 10)
