@@ -343,6 +343,8 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     static const int knobPair = std::getenv("GAR_HXS_PAIR") ? std::atoi(std::getenv("GAR_HXS_PAIR")) : 1;
     x.nt = knobNt;
     x.xcdPair = knobPair && fmt == 2 && (C / 16) % 2 == 0 && x.nblocks % 16 == 0 ? 1 : 0;
+    static const int knobChunkMajor = std::getenv("GAR_HXT_CHUNKMAJOR") ? std::atoi(std::getenv("GAR_HXT_CHUNKMAJOR")) : 1;
+    if (knobChunkMajor && fmt == 5 && x.nblocks % 8 == 0) x.xcdPair = 2;
     // output (o, c) at out + o*out_fs + c*out_cs bytes (o absolute)
     x.out_pcm = od.pcm;
     x.out_f64 = od.f64;

@@ -560,6 +560,14 @@ __device__ __forceinline__ void hxtLoaders(const HxsArgs& x, const HxsShared& sh
     }
 }
 
+// Workgroup slot -> block.  x.xcdPair 2 (FMT 5): chunk-major -- slot i runs block (i % 8) * (nblocks / 8) +
+// i / 8, so every channel group of a few consecutive chunks runs on one XCD (the dispatcher deals slots
+// round-robin over the 8 XCDs) and the 1-KB rows of those chunks are read and written together.
+__device__ __forceinline__ int hxtBlock(const HxsArgs& x, int i) {
+    if (x.xcdPair == 2) return (i & 7) * (x.nblocks >> 3) + (i >> 3);
+    return hxsBlock(x, i);
+}
+
 // ---- compute waves ----------------------------------------------------------------------
 // Group g: wait for its window, run this wave's periods p = first, first + st, ... < end
 // (chunk-relative), publish.  One accumulator pair per period: with three compute waves per SIMD
@@ -744,7 +752,7 @@ __global__ __launch_bounds__(64 * kHxtWaves) void hxt_kernel(HxsArgs x) {
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tBlockEnd = 0;
     for (int bi = blockIdx.x; bi < x.nblocks; bi += gridDim.x) {
-        const int b = hxsBlock(x, bi);
+        const int b = hxtBlock(x, bi);
         __syncthreads();  // the previous block's ring reads and fixup done
         if (threadIdx.x < NC) {
             s.loudLo[threadIdx.x] = INT_MAX;

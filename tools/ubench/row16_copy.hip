@@ -19,7 +19,7 @@ constexpr int kL = 6, kItems = 8;
 
 // MODE bit 1 loads, bit 2 stores; S16: 16-B stores; W: channels per workgroup (16 or 32).  256
 // workgroups: (kC / W) channel groups x (256 W / kC) chunks of the stream.
-template <int MODE, bool S16, int W, int MAP = 0>
+template <int MODE, int S16, int W, int MAP = 0>
 __global__ __launch_bounds__(1024) void k(const float* in, float* out) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int bi = blockIdx.x;
@@ -68,6 +68,15 @@ __global__ __launch_bounds__(1024) void k(const float* in, float* out) {
         const int sw = w - kL, nsw = (blockDim.x >> 6) - kL;
         const int grp = lane >> 4, l16 = lane & 15;
         for (int p = 0; p < np; ++p) {
+            if (S16 == 2) {  // W = 32: a row block's 16 rows x 32 channels as 8 dword stores of 2 whole 128-B rows
+                for (int t = sw; t < kPc / 16; t += nsw) {
+                    const long long row = (long long)p * kPc + 16 * t;
+                    float* ob = out + o0 * kC + W * g;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) ob[(row + 2 * i + (lane >> 5)) * kC + (lane & 31)] = acc + p + i;
+                }
+                continue;
+            }
             for (int t = sw; t < (kPc / 16) * (W / 16); t += nsw) {  // row block t % 10 of period p, column half t / 10
                 const int h = t / (kPc / 16), rb = t % (kPc / 16);
                 float* ob = out + o0 * kC + W * g + 16 * h;
@@ -103,18 +112,22 @@ int main() {
         printf("%-48s %8.3f ms  %.2f TB/s\n", name, ms / 5, bytes / (ms / 5 * 1e-3) / 1e12);
     };
     const int T = 64 * 16;
-    run(k<1, false, 16>, 256, T, (double)inB, "W16 loads only (6 loader waves)");
-    run(k<2, false, 16>, 256, T, (double)outB, "W16 stores only, 4x4-B per lane (VST 0)");
-    run(k<2, true, 16>, 256, T, (double)outB, "W16 stores only, 16-B per lane");
-    run(k<3, false, 16>, 256, T, (double)(inB + outB), "W16 loads + 4x4-B stores (ns256 pattern)");
-    run(k<3, true, 16>, 256, T, (double)(inB + outB), "W16 loads + 16-B stores");
-    run(k<1, false, 16, 1>, 256, T, (double)inB, "W16 chunk-major XCD map: loads only");
-    run(k<2, false, 16, 1>, 256, T, (double)outB, "W16 chunk-major XCD map: 4x4-B stores only");
-    run(k<3, false, 16, 1>, 256, T, (double)(inB + outB), "W16 chunk-major XCD map: loads + 4x4-B stores");
-    run(k<3, true, 16, 1>, 256, T, (double)(inB + outB), "W16 chunk-major XCD map: loads + 16-B stores");
-    run(k<1, false, 32>, 256, T, (double)inB, "W32 loads only (128-B rows)");
-    run(k<3, false, 32>, 256, T, (double)(inB + outB), "W32 loads + 4x4-B stores");
-    run(k<3, true, 32>, 256, T, (double)(inB + outB), "W32 loads + 16-B stores");
-    run(k<3, false, 32, 1>, 256, T, (double)(inB + outB), "W32 chunk-major XCD map: loads + 4x4-B stores");
+    run(k<1, 0, 16>, 256, T, (double)inB, "W16 loads only (6 loader waves)");
+    run(k<2, 0, 16>, 256, T, (double)outB, "W16 stores only, 4x4-B per lane (VST 0)");
+    run(k<2, 1, 16>, 256, T, (double)outB, "W16 stores only, 16-B per lane");
+    run(k<3, 0, 16>, 256, T, (double)(inB + outB), "W16 loads + 4x4-B stores (ns256 pattern)");
+    run(k<3, 1, 16>, 256, T, (double)(inB + outB), "W16 loads + 16-B stores");
+    run(k<1, 0, 16, 1>, 256, T, (double)inB, "W16 chunk-major XCD map: loads only");
+    run(k<2, 0, 16, 1>, 256, T, (double)outB, "W16 chunk-major XCD map: 4x4-B stores only");
+    run(k<3, 0, 16, 1>, 256, T, (double)(inB + outB), "W16 chunk-major XCD map: loads + 4x4-B stores");
+    run(k<3, 1, 16, 1>, 256, T, (double)(inB + outB), "W16 chunk-major XCD map: loads + 16-B stores");
+    run(k<1, 0, 32>, 256, T, (double)inB, "W32 loads only (128-B rows)");
+    run(k<3, 0, 32>, 256, T, (double)(inB + outB), "W32 loads + 4x4-B stores");
+    run(k<3, 1, 32>, 256, T, (double)(inB + outB), "W32 loads + 16-B stores");
+    run(k<3, 0, 32, 1>, 256, T, (double)(inB + outB), "W32 chunk-major XCD map: loads + 4x4-B stores");
+    run(k<2, 0, 32>, 256, T, (double)outB, "W32 stores only, 4x4-B per lane (64-B row halves)");
+    run(k<2, 2, 32>, 256, T, (double)outB, "W32 stores only, 2 whole rows per dword store");
+    run(k<3, 2, 32>, 256, T, (double)(inB + outB), "W32 loads + 2-whole-row dword stores");
+    run(k<3, 2, 32, 1>, 256, T, (double)(inB + outB), "W32 chunk-major: loads + 2-whole-row stores");
     return 0;
 }
