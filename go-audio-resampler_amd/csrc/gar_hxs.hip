@@ -187,7 +187,6 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     static const int knobG = std::getenv("GAR_HXS_G") ? std::atoi(std::getenv("GAR_HXS_G")) : 0;
     static const int knobWg = std::getenv("GAR_HXS_WGPERCU") ? std::atoi(std::getenv("GAR_HXS_WGPERCU")) : 0;
     static const bool trace = std::getenv("GAR_HX_TRACE") != nullptr;
-    static const int knobWide = std::getenv("GAR_HXT_WIDE") ? std::atoi(std::getenv("GAR_HXT_WIDE")) : 1;
     static const int knobDbg = std::getenv("GAR_HXS_DBG") ? std::atoi(std::getenv("GAR_HXS_DBG")) : 0;
     const int64_t Pc = p.Pc, Qc = p.Qc;
     const int64_t a_lo = fdiv(od.o_lo, Pc), a_hi = cdiv(od.o_hi, Pc);
@@ -202,8 +201,12 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     // 32-channel blocks of f32 rows on hxt_kernel (FMT 5, gar_hxt.hpp): whole 128-B lines per load and
     // store instruction; decided here (the chunk count depends on the block width), confirmed below
     const uintptr_t inA0 = reinterpret_cast<uintptr_t>(src.in);
-    bool wide = knobWide != 0 && !small && src.in && !src.in_pcm && !src.in_f64 && !od.pcm && !od.f64 && C % 32 == 0 &&
+    bool wide = !small && src.in && !src.in_pcm && !src.in_f64 && !od.pcm && !od.f64 && C % 32 == 0 &&
                 (inA0 & 15) == 0 && src.in_cs == 1 && src.in_fs % 4 == 0 && p.rb && p.nw <= kHxRbMaxWaves;
+    if (wide) {  // knob GAR_HXT_WIDE=0: 16-channel blocks (read per launch, so one test process compares both)
+        const char* e = std::getenv("GAR_HXT_WIDE");
+        wide = !e || std::atoi(e) != 0;
+    }
     const int bw = wide ? 32 : 16;
     // chunk length: about one block (bw columns) per CU
     const int64_t targetBlocks = static_cast<int64_t>(ncu) * (knobWg > 0 ? knobWg : 1);
