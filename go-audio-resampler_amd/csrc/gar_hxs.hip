@@ -201,11 +201,23 @@ hipError_t launchHxs(const HxDev& p, const SrcDesc& src, const OutDesc& od, int 
     // 32-channel blocks of f32 rows on hxt_kernel (FMT 5, gar_hxt.hpp): whole 128-B lines per load and
     // store instruction; decided here (the chunk count depends on the block width), confirmed below
     const uintptr_t inA0 = reinterpret_cast<uintptr_t>(src.in);
-    bool wide = !small && src.in && !src.in_pcm && !src.in_f64 && !od.pcm && !od.f64 && C % 32 == 0 &&
+    bool wide = !small && src.in && !src.in_pcm && !src.in_f64 && !od.pcm && !od.f64 && C % 32 == 0 && od.cs == 1 &&
                 (inA0 & 15) == 0 && src.in_cs == 1 && src.in_fs % 4 == 0 && p.rb && p.nw <= kHxRbMaxWaves;
     if (wide) {  // knob GAR_HXT_WIDE=0: 16-channel blocks (read per launch, so one test process compares both)
         const char* e = std::getenv("GAR_HXT_WIDE");
         wide = !e || std::atoi(e) != 0;
+    }
+    if (wide) {
+        // only where the 32-channel ring takes groups of >= 2 periods and the plan runs one compute wave per
+        // row block (balanced roles, NS = 10 as cfg3, measured slower on 32 channels) -- decided before the
+        // chunk count, which is sized for the block width (r06g: cfg3 fell back to 16-channel blocks after
+        // chunks sized for 32, 512 half-length blocks, traffic / algorithmic 1.06 -> 1.12, +7 %)
+        int rl[kHxtMaxComp] = {}, ms = 1;
+        const int nc = hxtRoles(p.nw, p.NS, rl, &ms);
+        int r2, rt2, wg2;
+        hxsRingFor(p, 2, r2, rt2, wg2);
+        wide = ms == 1 && hxtLdsWide(rt2) <= 160 * 1024 && 2 * Qc <= hxtMaxRowsF(5, nc + 6 <= kHxtWaves ? 6 : 4) &&
+               r2 / (2 * static_cast<int>(Qc)) + 3 <= kHxtSlots;
     }
     const int bw = wide ? 32 : 16;
     // chunk length: about one block (bw columns) per CU
