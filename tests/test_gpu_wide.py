@@ -71,6 +71,21 @@ def test_wide_blocks_bit_identical_and_vs_oracle(gar, O, cuda, ch, ir, orr, pres
         assert rms(wide[:, c], w) <= F32_RMS_TOL * max(1.0, float(np.abs(x[:, c]).max())), c
 
 
+@pytest.mark.parametrize("ch", [32, 64])
+def test_wide_blocks_history_seam_big_calls(gar, cuda, ch):
+    """Calls large enough for hxt_kernel after the first one (44.1k -> 48k, 2.5 s in calls of 0.9 s + a
+    ragged tail): each later call's first windows cross the history seam, which 32-channel blocks gather
+    through hxtGatherLoad over eight quads -- the bits equal the one-shot stream's and the 16-channel blocks'."""
+    torch = cuda
+    ir, orr = 44100, 48000
+    x = signal(int(2.5 * ir), ch, ir, seed=100 + ch).astype(np.float32).astype(np.float64)
+    x[int(1.2 * ir), ch // 2] = 25.0  # a loud sample right after the second call's seam
+    one = _device_run(gar, torch, x, ir, orr, 3)
+    wide, narrow = _both(gar, torch, x, ir, orr, 3, chunk=int(0.9 * ir) + 17)
+    assert _same_bits(wide, narrow)
+    assert _same_bits(wide, one)
+
+
 def test_wide_blocks_nonfinite_input(gar, O, cuda):
     """+Inf, -Inf and NaN samples in three channels of a 64-channel stream: the NaN / +Inf / -Inf class of
     every output equals the oracle's, and 32-channel blocks give the 16-channel blocks' bits."""
