@@ -827,11 +827,33 @@ def main():
         line["cpu_baseline"] = cpu_baseline(WORKLOADS[args.workload], target_s=args.cpu_baseline_seconds)
     if args.dry_run:
         line["dry_run"] = True
+    line["native_lib"] = native_lib_info()
     if rank == 0:
         print(json.dumps(front_keys(line)), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def native_lib_info():
+    """Provenance of the HIP library this run loaded: path, size, SHA-256 prefix, mtime, and whether it is
+    at least as new as every kernel / host source and the C ABI header it is built from (make's rule)."""
+    import hashlib
+    pkg = os.path.join(os.path.dirname(os.path.abspath(__file__)), "go-audio-resampler_amd")
+    path = os.environ.get("GAR_LIB_PATH") or os.path.join(pkg, "libgar.so")
+    if not os.path.exists(path):
+        return None
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    srcs = [os.path.join(pkg, "csrc", n) for n in os.listdir(os.path.join(pkg, "csrc"))]
+    srcs.append(os.path.join(os.path.dirname(pkg), "include", "gar.h"))
+    newest = max(os.path.getmtime(x) for x in srcs)
+    mt = os.path.getmtime(path)
+    return {"path": os.path.relpath(path, os.path.dirname(pkg)), "bytes": os.path.getsize(path),
+            "sha256_16": h.hexdigest()[:16], "mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(mt)),
+            "newer_than_sources": mt >= newest}
 
 
 def per_rank(obj, world):

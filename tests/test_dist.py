@@ -185,6 +185,10 @@ def test_bench_two_ranks_line_carries_cpu_baseline_and_per_rank():
     assert sorted(r["rank"] for r in d["per_rank"]) == [0, 1]
     assert all(r["local_ms_per_step"] is not None for r in d["per_rank"])
     assert sorted(r["rank"] for r in d["secondary"]["cfg4"]["per_rank"]) == [0, 1]
+    # build provenance: the library the run loaded, and whether make would rebuild it
+    nl = d["native_lib"]
+    assert nl["path"].endswith("libgar.so") and nl["bytes"] > 0 and len(nl["sha256_16"]) == 16
+    assert isinstance(nl["newer_than_sources"], bool)
 
 
 def test_bench_gpus_flag_conflicts_with_world_size():
