@@ -86,6 +86,18 @@ def test_wide_blocks_history_seam_big_calls(gar, cuda, ch):
     assert _same_bits(wide, one)
 
 
+@pytest.mark.parametrize("ch,seconds", [(32, 0.3), (160, 0.5), (224, 0.4), (96, 1.1)])
+def test_wide_blocks_odd_geometries(gar, cuda, ch, seconds):
+    """Channel counts whose block count is not a multiple of 8 (160, 224: the chunk-major slot order
+    is off) and streams short enough that few periods fall to each chunk (0.3 s of 32 channels: the
+    group-size fallback to 16-channel blocks): the bits equal the 16-channel blocks' either way."""
+    torch = cuda
+    ir, orr = 44100, 48000
+    x = signal(int(seconds * ir), ch, ir, seed=ch + 1).astype(np.float32).astype(np.float64)
+    wide, narrow = _both(gar, torch, x, ir, orr, 3)
+    assert _same_bits(wide, narrow)
+
+
 def test_wide_blocks_nonfinite_input(gar, O, cuda):
     """+Inf, -Inf and NaN samples in three channels of a 64-channel stream: the NaN / +Inf / -Inf class of
     every output equals the oracle's, and 32-channel blocks give the 16-channel blocks' bits."""
