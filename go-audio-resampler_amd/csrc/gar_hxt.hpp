@@ -572,6 +572,24 @@ __device__ __forceinline__ int hxtBlock(const HxsArgs& x, int i) {
 // Group g: wait for its window, run this wave's periods p = first, first + st, ... < end
 // (chunk-relative), publish.  One accumulator pair per period: with three compute waves per SIMD
 // the other waves cover a period's MFMA drain before its epilogue.
+// Stereo frame-pair stores (VST 2) of the fast epilogue as non-temporal stores (GAR_HXT_NTST2): the same
+// DPP frame-pair swap and 16-B store as hxsStoreFast<2>, with the nt cache policy.  In the headline's
+// memory pattern with no compute (tools/ubench/stereo_copy.hip, profiles/r06x4_stereo_copy_nt.txt) the
+// read and write streams together run at 4.77 TB/s with plain stores and 6.03 TB/s with nt stores.
+#ifndef GAR_HXT_NTST2
+#define GAR_HXT_NTST2 1
+#endif
+__device__ __forceinline__ void hxtStoreStereoNt(char* p, const f32x4& y, int lane) {
+    const bool even = (lane & 1) == 0;
+    const float s0 = even ? y[2] : y[0], s1 = even ? y[3] : y[1];
+    const float q0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s0), 0xB1, 0xf, 0xf, false));
+    const float q1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(s1), 0xB1, 0xf, 0xf, false));
+    f32x4 w;
+    if (even) { w[0] = y[0]; w[1] = q0; w[2] = y[1]; w[3] = q1; }
+    else      { w[0] = q0; w[1] = y[2]; w[2] = q1; w[3] = y[3]; }
+    __builtin_nontemporal_store(w, reinterpret_cast<f32x4*>(p));
+}
+
 // NT tiles per period (FMT 5: 2, the block's two 16-column halves, quads 4h .. 4h+3 of the ring and
 // channels ccol + 16h of the output; one accumulator pair per tile and period, in tile order).
 template <int NS, int VST, bool FAST, int NT = 1>
@@ -590,7 +608,9 @@ __device__ __forceinline__ void hxtGroups(const HxsArgs& x, const HxsShared& sh_
     auto epilogue = [&](const f32x4& oA, const f32x4& oL, int p, int h) {
         const f32x4 y = hxScale(oA, oL, sh);
         if (dbg & 2) return;
-        if constexpr (FAST) {
+        if constexpr (FAST && VST == 2 && GAR_HXT_NTST2) {
+            hxtStoreStereoNt(obase + static_cast<int64_t>(p) * pstride, y, lane);
+        } else if constexpr (FAST) {
             hxsStoreFast<VST>(x, obase + static_cast<int64_t>(p) * pstride + h * tileOut, y, lane);
         } else {
             const int ccol_ = ccol + 16 * h;

@@ -34,8 +34,15 @@ __global__ __launch_bounds__(1024) void k(const float* in, float* out) {
                 const int row = s * kG * kQc + 64 * pc + lane;
                 const bool on = s < kSteps && pc < kPieces && row < kChunkIn;
                 const int o = on ? (row + 2 * q * (int)kChunkIn) * 8 : (int)0x80000000u;
-                ra[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 0));
-                rb[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, on ? o + (int)kChunkIn * 8 : o, 0, 0));
+                if (MODE & 8) {  // non-temporal global loads (zeros for items past the chunk)
+                    const f2v* pa = reinterpret_cast<const f2v*>(base + (on ? o : 0));
+                    const f2v* pb = reinterpret_cast<const f2v*>(base + (on ? o + (int)kChunkIn * 8 : 0));
+                    ra[i] = on ? __builtin_nontemporal_load(pa) : f2v{0, 0};
+                    rb[i] = on ? __builtin_nontemporal_load(pb) : f2v{0, 0};
+                } else {
+                    ra[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 0));
+                    rb[i] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(rs, on ? o + (int)kChunkIn * 8 : o, 0, 0));
+                }
             }
         };
         issue(0, a[0], b[0]);
@@ -57,7 +64,8 @@ __global__ __launch_bounds__(1024) void k(const float* in, float* out) {
             for (int t = sw; t < kPc / 16; t += nsw) {
                 const long long frame = o0 + ck * kChunkOut + (long long)p * kPc + 16 * t + fr;
                 const f32x4 y = {acc + p, acc + t, acc, acc};
-                *reinterpret_cast<f32x4*>(out + 2 * frame) = y;
+                if (MODE & 4) __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(out + 2 * frame));
+                else *reinterpret_cast<f32x4*>(out + 2 * frame) = y;
             }
     }
 }
@@ -84,5 +92,9 @@ int main() {
     run(k<1>, (double)inB, "loads only (6 loader waves)");
     run(k<2>, (double)outB, "stores only (10 waves, 16 B per lane)");
     run(k<3>, (double)(inB + outB), "loads + stores (cfg2 pattern)");
+    run(k<7>, (double)(inB + outB), "loads + non-temporal stores");
+    run(k<11>, (double)(inB + outB), "non-temporal loads + stores");
+    run(k<15>, (double)(inB + outB), "non-temporal loads + nt stores");
+    run(k<3>, (double)(inB + outB), "loads + stores (again)");
     return 0;
 }
